@@ -1,0 +1,136 @@
+/*
+ * phylo_hip.h -- C-ABI of the MI355X Felsenstein-pruning likelihood engine.
+ *
+ * This is the drop-in boundary that replaces phylostan's likelihood hot path
+ * (SURVEY.md 8b).  In the reference the same role is played by
+ *
+ *   - the Stan external function declared without a body
+ *       real pruning_loglik(vector blens);            eigen/example.stan:3
+ *     with its double overload (eigen/eigen.j2:171-177) and its autodiff
+ *     overload returning precomputed_gradients(log_P, blens, grad)
+ *       (eigen/prune_stan.hpp:9-17), backed by
+ *       value_grad vbsky_loglik(const vector<double>& times)
+ *       (eigen/eigen.j2:56-168; struct value_grad eigen/value_grad.hpp:5-8),
+ *   - and, for the generated models, the Stan code emitted by
+ *       phylostan/generate_script.py:961-1055 (likelihood loop),
+ *       :755-892 (JC69 / HKY / GTR P-matrices) and
+ *       :249-282 (Weibull site rates -> rs, ps),
+ *     differentiated by Stan's reverse-mode autodiff.
+ *
+ * Plain C types only: pointers + sizes, no torch / HIP types in signatures.
+ * Every function returns 0 on success and a nonzero PHY_E* code on misuse or
+ * a HIP failure; phy_last_error() then returns a message (thread-local).
+ * A non-finite log-likelihood is NOT an error: it is returned as -inf with
+ * status 0 so a sampler rejects the draw, as Stan does.
+ *
+ * Conventions (identical to the reference's, minus one for 0-based ids):
+ *   S taxa, P site patterns, C rate categories.
+ *   Node ids: tips 0..S-1 in taxon-namespace order, internal S..2S-2 in
+ *     post-order, root 2S-2   (phylostan/utils.py:59-72).
+ *   peel[(S-1)*3]: rows (child1, child2, parent), post-order
+ *     (phylostan/utils.py:75-81).  Unrooted (no clock) trees: the last row's
+ *     child2 must be node 2S-3, whose branch is merged into child1's
+ *     (phylostan/phylostan.py:264-267, generate_script.py:1019).
+ *   B = 2S-2 branches (rooted) or 2S-3 (unrooted); branch b is the edge
+ *     above node b, so blens[b] == Stan blens[b+1]
+ *     (generate_script.py:1193-1196, :663-671).
+ *   tipcodes[S*P]: 4-bit state masks, A=1 C=2 G=4 T=8; any other symbol 15
+ *     (the reference's [1,1,1,1], phylostan/utils.py:180-187).
+ *   Per-draw model vector, length PHY_MODEL_LEN(C) = 10 + 2C:
+ *     [0..3]  freqs (pi_A, pi_C, pi_G, pi_T)
+ *     [4..9]  exchangeabilities AC, AG, AT, CG, CT, GT (GTR; HKY passes
+ *             (1,kappa,1,1,kappa,1), generate_script.py:799-802; JC69 ignores)
+ *     [10..10+C)     rs  (category rates)
+ *     [10+C..10+2C)  ps  (category weights)
+ *   Per-draw output vector, length phy_output_len() = 1 + B + 2C + 4 + 16*C*B:
+ *     [0]                 log-likelihood  sum_i w_i log L_i
+ *     [1 .. 1+B)          dlogL/dblens
+ *     [1+B .. 1+B+C)      dlogL/drs
+ *     [1+B+C .. 1+B+2C)   dlogL/dps
+ *     [1+B+2C .. +4)      dlogL/dfreqs, explicit root term only
+ *     [PHY_OUT_G(B,C) ..) dlogL/dP[c][b][4][4] (row-major P[j][k]); index
+ *                         c*B + b is Stan's pmats[b + c*bcount]
+ */
+#ifndef PHYLO_HIP_H
+#define PHYLO_HIP_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct phy_ctx phy_ctx;
+
+enum { PHY_JC69 = 0, PHY_HKY = 1, PHY_GTR = 2 };
+
+enum {
+  PHY_OK = 0,
+  PHY_EINVAL = 1,   /* bad argument / inconsistent topology */
+  PHY_EHIP = 2,     /* HIP runtime failure */
+  PHY_ENOMEM = 3,   /* device allocation failed */
+  PHY_ERANGE = 4    /* n_draws > max_draws etc. */
+};
+
+#define PHY_MODEL_LEN(C) (10 + 2 * (C))
+#define PHY_OUT_G(B, C) (1 + (B) + 2 * (C) + 4)
+
+/* Build a context: copies the static data (tips, weights, topology) to the
+ * device, derives the kernel traversal program and allocates every work
+ * buffer.  Replaces the compile-time baking of topology / tips / Q into the
+ * generated header (eigen/util.py:103-109, eigen/eigen.j2:19-38) and the
+ * Stan data block (generate_script.py:1186-1197).
+ *   rooted: 1 = clock variants (:984-1012), 0 = unrooted (:1013-1040).
+ *   max_draws: most independent parameter points one phy_eval may batch.
+ *   device: HIP device ordinal (one process per GPU). */
+int phy_create(int S, int P, int C, int rooted, int model,
+               const uint8_t* tipcodes, const double* weights, const int32_t* peel,
+               int max_draws, int device, phy_ctx** out);
+
+int phy_destroy(phy_ctx* ctx);
+
+/* Message of the last failure on this thread ("" if none). */
+const char* phy_last_error(void);
+
+int phy_num_branches(const phy_ctx* ctx);
+int phy_output_len(const phy_ctx* ctx);
+/* Traversal-program facts: steps (= S-1), partial slots, LDS stack depth,
+ * pattern blocks of 64. */
+int phy_program_info(const phy_ctx* ctx, int* nsteps, int* nslots, int* depth, int* nblocks);
+
+/* Log-likelihood + full gradient of n_draws parameter points, host buffers,
+ * synchronous.  blens[n_draws*B], model[n_draws*PHY_MODEL_LEN(C)],
+ * out[n_draws*phy_output_len()], site_ll[n_draws*P] (per-site log L_i, may
+ * be NULL).  The batched analogue of vbsky_loglik (eigen/eigen.j2:56). */
+int phy_eval(phy_ctx* ctx, int n_draws, const double* blens, const double* model,
+             double* out, double* site_ll);
+
+/* Same, device buffers, asynchronous on `stream` (a hipStream_t; NULL =
+ * the context's own stream).  Nothing is copied to or from the host. */
+int phy_eval_device(phy_ctx* ctx, int n_draws, const double* d_blens, const double* d_model,
+                    double* d_out, double* d_site_ll, void* stream);
+
+/* Mirror of the reference's external Stan function: the double overload
+ * returns log P (eigen/eigen.j2:171-177); with grad != NULL it also fills
+ * dlogL/dblens[B] -- the `grads` that prune_stan.hpp:16 hands to
+ * precomputed_gradients.  Returns NaN (and sets phy_last_error) on misuse. */
+double phy_pruning_loglik(phy_ctx* ctx, const double* blens, const double* model, double* grad);
+
+/* Wait for all work of the context's stream. */
+int phy_sync(phy_ctx* ctx);
+
+/* Measurement hooks (bench.py): while enabled, every phy_eval* records HIP
+ * events around the sweep kernel on the stream it runs on;
+ * phy_timing_read synchronises and returns the summed sweep-kernel time in
+ * ms and the number of launches since phy_timing_start. */
+int phy_timing_start(phy_ctx* ctx);
+int phy_timing_read(phy_ctx* ctx, double* total_ms, int* launches);
+
+/* Tuning: persistent workgroup budget per launch (0 = default) and where the
+ * dL/dP partial sums live (0 auto, 1 LDS, 2 global). */
+int phy_set_tuning(phy_ctx* ctx, int wg_budget, int g_mode);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* PHYLO_HIP_H */

@@ -1,0 +1,73 @@
+"""ctypes binding of the C-ABI in ``include/phylo_hip.h``.
+
+This is the Python-side binding a maintainer would add to the reference in
+place of its Stan external-function plumbing (``eigen/util.py:113-129`` /
+``eigen/prune_stan.hpp``): the shared library is loaded once, every entry
+point gets an explicit signature, and a missing library is a hard error --
+there is no CPU fallback in the product path.
+"""
+import ctypes
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libphylo_hip.so")
+
+PHY_JC69, PHY_HKY, PHY_GTR = 0, 1, 2
+
+_lib = None
+
+_c_double_p = ctypes.POINTER(ctypes.c_double)
+_c_int_p = ctypes.POINTER(ctypes.c_int)
+
+# name -> (restype, argtypes)
+SIGNATURES = {
+    "phy_create": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                  ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int,
+                                  ctypes.c_int, ctypes.POINTER(ctypes.c_void_p)]),
+    "phy_destroy": (ctypes.c_int, [ctypes.c_void_p]),
+    "phy_last_error": (ctypes.c_char_p, []),
+    "phy_num_branches": (ctypes.c_int, [ctypes.c_void_p]),
+    "phy_output_len": (ctypes.c_int, [ctypes.c_void_p]),
+    "phy_program_info": (ctypes.c_int, [ctypes.c_void_p, _c_int_p, _c_int_p, _c_int_p, _c_int_p]),
+    "phy_eval": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p,
+                                ctypes.c_void_p, ctypes.c_void_p]),
+    "phy_eval_device": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p,
+                                       ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
+    "phy_pruning_loglik": (ctypes.c_double, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                             ctypes.c_void_p]),
+    "phy_sync": (ctypes.c_int, [ctypes.c_void_p]),
+    "phy_timing_start": (ctypes.c_int, [ctypes.c_void_p]),
+    "phy_timing_read": (ctypes.c_int, [ctypes.c_void_p, _c_double_p, _c_int_p]),
+    "phy_set_tuning": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_int]),
+}
+
+
+class PhyloHipError(RuntimeError):
+    pass
+
+
+def load(path=None):
+    """Load (once) and return the library.  Raises ``PhyloHipError`` if the
+    HIP library has not been built -- the product has no CPU fallback."""
+    global _lib
+    if _lib is not None and path is None:
+        return _lib
+    p = path or LIB_PATH
+    if not os.path.exists(p):
+        raise PhyloHipError(
+            "HIP library %s is missing: build it with `python -c 'import __graft_entry__ as g; g.build()'` "
+            "(there is no CPU fallback in phylostan_amd)" % p)
+    lib = ctypes.CDLL(p)
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    if path is None:
+        _lib = lib
+    return lib
+
+
+def check(rc, what):
+    if rc != 0:
+        msg = load().phy_last_error().decode(errors="replace")
+        raise PhyloHipError("%s failed (code %d): %s" % (what, rc, msg))

@@ -1,0 +1,169 @@
+"""Host-side mirror of the reference's likelihood interface over the C-ABI.
+
+In phylostan the likelihood is reached two ways, both replaced here:
+
+* the emitted Stan model block -- data dict ``{peel, tipdata, weights, C,
+  map, ...}`` (``phylostan/phylostan.py:181-286``) and parameters; the model
+  block computes ``pmats`` (``generate_script.py:1425/1439/1447``) then
+  ``target += log(sum(probs)) * weights[i]`` (``:961-1055``), and Stan's
+  autodiff supplies the gradient;
+* the external-function plugin ``real pruning_loglik(vector blens)``
+  (``eigen/example.stan:3``, ``eigen/prune_stan.hpp:9-17``) returning the
+  value and ``precomputed_gradients``.
+
+``TreeLikelihood`` owns one ``phy_ctx`` (one GPU, one process); its
+``log_prob`` / ``pruning_loglik`` return the value and the gradient the
+Stan model would have produced.  There is no CPU fallback: without the HIP
+library ``_lib.load()`` raises.
+"""
+import ctypes
+
+import numpy as np
+
+from . import _lib
+from . import models
+
+
+class EvalResult:
+    """Unpacked output vector of one draw (layout: include/phylo_hip.h)."""
+
+    __slots__ = ("loglik", "grad_blens", "grad_rs", "grad_ps", "grad_freq_root", "dLdP",
+                 "site_ll")
+
+    def __init__(self, vec, B, C, site_ll=None):
+        og = 1 + B + 2 * C + 4
+        self.loglik = float(vec[0])
+        self.grad_blens = vec[1:1 + B].copy()
+        self.grad_rs = vec[1 + B:1 + B + C].copy()
+        self.grad_ps = vec[1 + B + C:1 + B + 2 * C].copy()
+        self.grad_freq_root = vec[1 + B + 2 * C:og].copy()
+        self.dLdP = vec[og:og + C * B * 16].reshape(C, B, 4, 4).copy()
+        self.site_ll = site_ll
+
+    def as_dict(self):
+        return {k: getattr(self, k) for k in self.__slots__}
+
+
+def _ptr(a):
+    return a.ctypes.data_as(ctypes.c_void_p)
+
+
+class TreeLikelihood:
+    """GPU pruning likelihood of one alignment + topology.
+
+    Parameters
+    ----------
+    tipcodes : uint8 [S, P] state masks (A=1, C=2, G=4, T=8, other 15)
+    weights  : [P] pattern multiplicities
+    peel0    : int [S-1, 3] 0-based peel rows (child1, child2, parent)
+    rooted   : True for the clock (rooted) model variants
+    model    : "JC69" | "HKY" | "GTR"
+    C        : rate categories
+    max_draws: parameter points per batched evaluation
+    device   : HIP device ordinal
+    """
+
+    def __init__(self, tipcodes, weights, peel0, rooted, model, C, max_draws=1, device=0):
+        self.lib = _lib.load()
+        tipcodes = np.ascontiguousarray(tipcodes, dtype=np.uint8)
+        self.S, self.P = tipcodes.shape
+        self.C = int(C)
+        self.rooted = bool(rooted)
+        self.model = models.MODEL_IDS[model] if isinstance(model, str) else int(model)
+        self.max_draws = int(max_draws)
+        w = np.ascontiguousarray(weights, dtype=np.float64)
+        peel = np.ascontiguousarray(peel0, dtype=np.int32)
+        if w.shape != (self.P,):
+            raise ValueError("weights must have shape (P,)")
+        if peel.shape != (self.S - 1, 3):
+            raise ValueError("peel must have shape (S-1, 3)")
+        ctx = ctypes.c_void_p()
+        _lib.check(self.lib.phy_create(self.S, self.P, self.C, int(self.rooted), self.model,
+                                       _ptr(tipcodes), _ptr(w), _ptr(peel), self.max_draws,
+                                       int(device), ctypes.byref(ctx)), "phy_create")
+        self.ctx = ctx
+        self.B = self.lib.phy_num_branches(ctx)
+        self.outlen = self.lib.phy_output_len(ctx)
+        self.model_len = 10 + 2 * self.C
+
+    @classmethod
+    def from_data(cls, data, model, C, **kw):
+        """From a ``phylostan_amd.data.PhyloData`` (what ``phylostan run``
+        builds before handing the dict to Stan)."""
+        return cls(data.tipcodes, data.weights, data.peel0, data.rooted, model, C, **kw)
+
+    def close(self):
+        if getattr(self, "ctx", None):
+            self.lib.phy_destroy(self.ctx)
+            self.ctx = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def program_info(self):
+        vals = [ctypes.c_int() for _ in range(4)]
+        _lib.check(self.lib.phy_program_info(self.ctx, *[ctypes.byref(v) for v in vals]),
+                   "phy_program_info")
+        return dict(zip(("nsteps", "nslots", "depth", "nblocks"), [v.value for v in vals]))
+
+    def model_vector(self, freqs, rates, rs, ps):
+        v = models.model_vector(freqs, rates, rs, ps)
+        if v.shape != (self.model_len,):
+            raise ValueError("model vector must have length 10 + 2C")
+        return v
+
+    def evaluate_batch(self, blens, model_vecs, site_ll=False):
+        """n draws: blens [n, B], model_vecs [n, 10+2C] -> list of EvalResult."""
+        blens = np.ascontiguousarray(np.atleast_2d(blens), dtype=np.float64)
+        mv = np.ascontiguousarray(np.atleast_2d(model_vecs), dtype=np.float64)
+        n = blens.shape[0]
+        if blens.shape != (n, self.B) or mv.shape != (n, self.model_len):
+            raise ValueError("bad shapes: blens %s model %s" % (blens.shape, mv.shape))
+        out = np.empty((n, self.outlen))
+        sl = np.empty((n, self.P)) if site_ll else None
+        _lib.check(self.lib.phy_eval(self.ctx, n, _ptr(blens), _ptr(mv), _ptr(out),
+                                     _ptr(sl) if site_ll else None), "phy_eval")
+        return [EvalResult(out[k], self.B, self.C, sl[k] if site_ll else None) for k in range(n)]
+
+    def evaluate(self, blens, model_vec, site_ll=False):
+        return self.evaluate_batch(blens, model_vec, site_ll)[0]
+
+    def evaluate_device(self, d_blens, d_model, d_out, d_site_ll=0, n_draws=1, stream=0):
+        """Device-pointer path (ints), asynchronous on ``stream``."""
+        _lib.check(self.lib.phy_eval_device(self.ctx, int(n_draws), ctypes.c_void_p(d_blens),
+                                            ctypes.c_void_p(d_model), ctypes.c_void_p(d_out),
+                                            ctypes.c_void_p(d_site_ll) if d_site_ll else None,
+                                            ctypes.c_void_p(stream) if stream else None),
+                   "phy_eval_device")
+
+    def pruning_loglik(self, blens, model_vec):
+        """``pruning_loglik(blens)`` of eigen/prune_stan.hpp:9-17: returns
+        ``(log_P, grad)`` -- the value and the precomputed gradient."""
+        blens = np.ascontiguousarray(blens, dtype=np.float64)
+        mv = np.ascontiguousarray(model_vec, dtype=np.float64)
+        grad = np.empty(self.B)
+        val = self.lib.phy_pruning_loglik(self.ctx, _ptr(blens), _ptr(mv), _ptr(grad))
+        if np.isnan(val):
+            msg = self.lib.phy_last_error().decode(errors="replace")
+            if msg:
+                raise _lib.PhyloHipError("phy_pruning_loglik: " + msg)
+        return val, grad
+
+    def sync(self):
+        _lib.check(self.lib.phy_sync(self.ctx), "phy_sync")
+
+    def set_tuning(self, wg_budget=0, g_mode=0):
+        _lib.check(self.lib.phy_set_tuning(self.ctx, int(wg_budget), int(g_mode)), "phy_set_tuning")
+
+    def timing_start(self):
+        _lib.check(self.lib.phy_timing_start(self.ctx), "phy_timing_start")
+
+    def timing_read(self):
+        ms = ctypes.c_double()
+        n = ctypes.c_int()
+        _lib.check(self.lib.phy_timing_read(self.ctx, ctypes.byref(ms), ctypes.byref(n)),
+                   "phy_timing_read")
+        return ms.value, n.value

@@ -1,0 +1,159 @@
+#!/usr/bin/env python
+"""Regenerate the golden fixtures in tests/golden/ from the REFERENCE itself.
+
+Run in the build container (the reference is mounted at /root/reference; it
+does not exist on the GPU box, so the fixtures are committed):
+
+    python tests/golden/make_golden.py
+
+What is taken from the reference (nothing here is restated by us):
+
+* ``kat_3tax.json`` -- the closed-form 3-taxon JC log-likelihood of
+  ``eigen/test_ll_3tax.py:22-320`` evaluated at the two points the script
+  uses (``:323-329``), plus central finite-difference gradients of that same
+  formula.  jax is absent, so ``jax`` / ``jax.numpy`` are bound to numpy for
+  the duration of the import (the formula only calls ``exp`` and ``log``).
+* ``<dataset>_layout.npz`` -- the Stan data layout that ``phylostan run``
+  builds: ``phylostan/utils.py`` functions ``setup_indexes``,
+  ``setup_dates``, ``get_peeling_order``, ``get_preorder``, ``get_lowers``
+  and ``get_dna_leaves_partials_compressed`` are imported from the reference
+  and run on the example inputs.  DendroPy is absent, so the tree / alignment
+  objects they walk are our own DendroPy-compatible ones
+  (``phylostan_amd/treeio.py``); ``numpy.int`` (removed in numpy >= 1.24) is
+  re-bound to ``int`` for the call.  ``tipdata`` (0/1 ``[S, L, 4]``) is
+  stored losslessly as bit masks ``sum_k tipdata[..., k] << k``.
+"""
+import json
+import os
+import sys
+import types
+
+import numpy as np
+
+REF = "/root/reference"
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, REPO)
+
+from phylostan_amd import treeio  # noqa: E402
+
+
+def _import_reference_utils():
+    sys.path.insert(0, REF)
+    import numpy
+    if not hasattr(numpy, "int"):
+        numpy.int = int
+    from phylostan import utils  # noqa: E402  (pure python, needs numpy only)
+    return utils
+
+
+def kat_fixture():
+    fake_jax = types.ModuleType("jax")
+    fake_jax.numpy = np
+    sys.modules["jax"] = fake_jax
+    sys.modules["jax.numpy"] = np
+    sys.path.insert(0, os.path.join(REF, "eigen"))
+    import test_ll_3tax  # noqa: E402
+    f = test_ll_3tax.loglik3tax
+    mu = 1.0
+    pi = np.ones(4) / 4
+    tips = np.eye(4)[:3]
+    points = []
+    for times in ([1.0, 1.0, 1.0, 1.0], [0.1, 0.1, 0.2, 0.3]):
+        t = np.array(times)
+        ll = float(f(mu, pi, tips, t))
+        h = 1e-6
+        grad = []
+        for k in range(4):
+            tp, tm = t.copy(), t.copy()
+            tp[k] += h
+            tm[k] -= h
+            grad.append((float(f(mu, pi, tips, tp)) - float(f(mu, pi, tips, tm))) / (2 * h))
+        points.append({"branches_b14_b24_b45_b35": times, "loglik": ll, "grad_fd": grad})
+    del sys.modules["jax"], sys.modules["jax.numpy"]
+    return {
+        "source": "eigen/test_ll_3tax.py:22-329 (reference closed form, evaluated with numpy)",
+        "tree": "((1:b14,2:b24)4:b45,3:b35)5",
+        "tips": "A, C, G (eye(4)[:3])",
+        "Q": "JC unnormalised: off-diagonal 0.25, diagonal -0.75 (eigen/util.py:96-99); "
+             "P(t) = 0.25 + 0.75 exp(-t) on the diagonal, so t_eigen = b_stan / 0.75",
+        "points": points,
+    }
+
+
+class _Seq(str):
+    def symbols_as_string(self):
+        return str(self)
+
+
+class _Alignment(dict):
+    """What get_dna_leaves_partials_compressed touches of a DendroPy
+    DnaCharacterMatrix: iteration in taxon-namespace order, ``[name][i]``,
+    ``symbols_as_string()``, ``sequence_size``."""
+
+    def __init__(self, rows):
+        super().__init__(rows)
+        self.sequence_size = len(next(iter(rows.values())))
+
+
+def layout_fixture(utils, tree_path, aln_path, heterochronous, rooted):
+    tree = treeio.read_tree(tree_path)
+    tree.resolve_polytomies(update_bipartitions=True)
+    utils.setup_indexes(tree)
+    oldest = utils.setup_dates(tree, None, heterochronous)
+    peel = utils.get_peeling_order(tree)
+    if not rooted:  # phylostan.py:264-267
+        last = peel[-1]
+        if last[0] > last[1]:
+            peel[-1] = [last[1], last[0], last[2]]
+    pre = utils.get_preorder(tree)
+    aln = treeio.read_alignment(aln_path)
+    rows = {t.label: _Seq(aln[t.label]) for t in tree.taxon_namespace}
+    tipdata, weights = utils.get_dna_leaves_partials_compressed(_Alignment(rows))
+    tipdata = np.asarray(tipdata)
+    bits = (tipdata * (1 << np.arange(4))).sum(-1).astype(np.uint8)
+    out = dict(tipbits=bits, weights=np.asarray(weights, dtype=np.int64),
+               peel=np.asarray(peel, dtype=np.int32), map=np.asarray(pre, dtype=np.int32),
+               taxa=np.array([t.label for t in tree.taxon_namespace]),
+               sites=np.int64(len(next(iter(aln.values())))))
+    if heterochronous:
+        out["lowers"] = np.asarray(utils.get_lowers(tree), dtype=np.float64)
+        out["oldest"] = np.float64(oldest)
+    # node heights implied by the input tree (used for fluA / HCV parameter
+    # points: blens = rate * (h[parent] - h[node]), generate_script.py:660-679)
+    S = len(tree.taxon_namespace)
+    if any(n.edge_length is None for n in tree.postorder_node_iter() if n.parent_node is not None):
+        return out  # topology-only tree (DS1)
+    h = {}
+    for node in tree.postorder_node_iter():
+        h[node] = node.date if node.is_leaf() else max(h[c] + c.edge_length for c in node.child_node_iter())
+    heights = np.zeros(S - 1)
+    dates = np.zeros(S)
+    for node in tree.postorder_node_iter():
+        if node.is_leaf():
+            dates[node.index - 1] = node.date
+        else:
+            heights[node.index - S - 1] = h[node]
+    out["heights"] = heights
+    out["tip_dates"] = dates
+    return out
+
+
+def main():
+    with open(os.path.join(HERE, "kat_3tax.json"), "w") as fp:
+        json.dump(kat_fixture(), fp, indent=1)
+    utils = _import_reference_utils()
+    ex = os.path.join(REF, "examples")
+    specs = {
+        "fluA": (os.path.join(ex, "fluA", "fluA.tree"), os.path.join(ex, "fluA", "fluA.fa"), True, True),
+        "HCV": (os.path.join(ex, "HCV", "HCV.tree"), os.path.join(ex, "HCV", "HCV.nexus"), False, True),
+        "DS1": (os.path.join(ex, "DS1", "DS1.trees"), os.path.join(ex, "DS1", "DS1.nex"), False, False),
+    }
+    for name, (tpath, apath, het, rooted) in specs.items():
+        fx = layout_fixture(utils, tpath, apath, het, rooted)
+        np.savez_compressed(os.path.join(HERE, "%s_layout.npz" % name), **fx)
+        print(name, "S=%d P=%d sites=%d" % (fx["tipbits"].shape[0], fx["tipbits"].shape[1], fx["sites"]))
+
+
+if __name__ == "__main__":
+    main()

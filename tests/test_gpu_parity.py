@@ -1,0 +1,158 @@
+"""GPU parity: the HIP path (through the C-ABI) against the CPU oracle.
+
+Tolerances (north_star: per-site log-likelihoods within 1e-6 relative of the
+reference; we hold the HIP path to far tighter):
+  per-site log L and total log L:  rel 1e-10 (+ abs 1e-12)
+  gradients (dL/dP, blens, rs, ps, root freqs): rel 1e-9 of the largest
+  entry's magnitude per array.
+"""
+import numpy as np
+import pytest
+
+from tests import cases
+
+pytestmark = pytest.mark.gpu
+
+RTOL_LL = 1e-10
+RTOL_G = 1e-9
+
+
+def _engine(case, max_draws=1, **kw):
+    from phylostan_amd.engine import TreeLikelihood
+    return TreeLikelihood(case.tipcodes, case.weights, case.peel0, case.rooted, case.model, case.C,
+                          max_draws=max_draws, **kw)
+
+
+def _close(a, b, rtol, what):
+    a = np.asarray(a, dtype=np.float64)
+    b = np.asarray(b, dtype=np.float64)
+    scale = max(np.max(np.abs(b)), 1e-300)
+    err = np.max(np.abs(a - b)) / scale
+    assert err <= rtol, "%s: max rel err %.3e > %.1e" % (what, err, rtol)
+
+
+def check_case(case, eng=None, res=None):
+    eng = eng or _engine(case)
+    if res is None:
+        res = eng.evaluate(case.blens, case.model_vec(), site_ll=True)
+    ref = case.oracle()
+    np.testing.assert_allclose(res.site_ll, ref["site_ll"], rtol=RTOL_LL, atol=1e-12)
+    assert abs(res.loglik - ref["loglik"]) <= RTOL_LL * abs(ref["loglik"]) + 1e-12
+    _close(res.dLdP, ref["dLdP"], RTOL_G, "dLdP")
+    _close(res.grad_blens, ref["grad_blens"], RTOL_G, "grad_blens")
+    _close(res.grad_rs, ref["grad_rs"], RTOL_G, "grad_rs")
+    _close(res.grad_ps, ref["grad_ps"], RTOL_G, "grad_ps")
+    _close(res.grad_freq_root, ref["grad_freq_root"], RTOL_G, "grad_freq_root")
+    return res
+
+
+def test_kat_3tax_reference_values():
+    """The reference's only known-answer test (eigen/test_ll_3tax.py)."""
+    kat = cases.load_kat()
+    for pt in kat["points"]:
+        case = cases.kat_case(pt)
+        res = check_case(case)
+        assert abs(res.loglik - pt["loglik"]) < 1e-12
+        g = res.grad_blens * 0.75  # d/dt of the unnormalised-Q formula
+        np.testing.assert_allclose(g[[0, 1, 3, 2]], pt["grad_fd"], rtol=1e-6)
+
+
+@pytest.mark.parametrize("make", [cases.fluA_case, cases.hcv_case, cases.ds1_case],
+                         ids=["fluA_HKY_W4", "HCV_GTR_W4", "DS1_JC69_unrooted"])
+def test_config_datasets(make):
+    check_case(make())
+
+
+@pytest.mark.parametrize("seed,S,P,C,model,rooted,cat", [
+    (1, 5, 1, 1, "JC69", True, False),       # single pattern
+    (2, 12, 63, 3, "GTR", True, False),      # P < one block
+    (3, 12, 130, 4, "HKY", True, False),     # ragged last block
+    (4, 17, 257, 5, "GTR", False, False),    # unrooted, C=5 (+I-like)
+    (5, 40, 200, 2, "GTR", True, True),      # caterpillar (deep tree)
+    (6, 40, 200, 4, "JC69", False, True),    # unrooted caterpillar
+    (7, 128, 300, 4, "GTR", True, False),    # synthetic-config taxa
+    (8, 9, 100, 8, "HKY", True, False),      # C=8 -> 512-thread workgroups
+])
+def test_random_trees(seed, S, P, C, model, rooted, cat):
+    check_case(cases.random_case(seed, S=S, P=P, C=C, model=model, rooted=rooted, caterpillar=cat))
+
+
+def test_all_ambiguous_and_padding():
+    case = cases.random_case(11, S=10, P=70, C=2, ambiguous=1.0)
+    check_case(case)
+
+
+@pytest.mark.parametrize("g_mode", [1, 2])
+def test_g_modes(g_mode):
+    case = cases.fluA_case()
+    eng = _engine(case)
+    eng.set_tuning(0, g_mode)
+    check_case(case, eng)
+
+
+def test_batched_draws_match_single():
+    base = cases.fluA_case()
+    rng = np.random.default_rng(3)
+    n = 7
+    eng = _engine(base, max_draws=n)
+    blens = base.blens[None, :] * rng.uniform(0.5, 1.5, (n, 1))
+    mvs = []
+    for k in range(n):
+        kappa = rng.uniform(2, 9)
+        mvs.append(cases.models.model_vector(base.freqs, cases.models.hky_exchangeabilities(kappa),
+                                             base.rs, base.ps))
+    res = eng.evaluate_batch(blens, np.array(mvs), site_ll=True)
+    for k in range(n):
+        c = cases.Case("d%d" % k, base.tipcodes, base.weights, base.peel0, True, "HKY", 4, blens[k],
+                       base.freqs, mvs[k][4:10], base.rs, base.ps)
+        check_case(c, eng, res[k])
+
+
+def test_persistent_workgroups_loop():
+    """Fewer workgroups than pattern blocks: every workgroup loops."""
+    case = cases.random_case(21, S=20, P=64 * 9 + 5, C=3)
+    eng = _engine(case)
+    eng.set_tuning(2, 0)
+    check_case(case, eng)
+
+
+def test_deterministic():
+    case = cases.hcv_case()
+    eng = _engine(case)
+    a = eng.evaluate(case.blens, case.model_vec(), site_ll=True)
+    b = eng.evaluate(case.blens, case.model_vec(), site_ll=True)
+    assert a.loglik == b.loglik
+    assert np.array_equal(a.dLdP, b.dLdP) and np.array_equal(a.site_ll, b.site_ll)
+
+
+def test_pruning_loglik_mirror():
+    case = cases.ds1_case(1)
+    eng = _engine(case)
+    val, grad = eng.pruning_loglik(case.blens, case.model_vec())
+    ref = case.oracle()
+    assert abs(val - ref["loglik"]) <= 1e-10 * abs(ref["loglik"])
+    _close(grad, ref["grad_blens"], RTOL_G, "grad")
+
+
+def test_nonfinite_is_minus_inf():
+    case = cases.random_case(5, S=6, P=10, C=1, model="JC69")
+    eng = _engine(case)
+    mv = case.model_vec()
+    mv[10 + case.C:] = 0.0  # ps = 0 -> L = 0 -> log L = -inf
+    res = eng.evaluate(case.blens, mv)
+    assert res.loglik == -np.inf
+
+
+def test_errors_are_loud():
+    from phylostan_amd._lib import PhyloHipError
+    case = cases.random_case(5, S=6, P=10, C=1, model="JC69")
+    bad = case.peel0.copy()
+    bad[0, 0] = 99
+    with pytest.raises(PhyloHipError):
+        cases.Case("bad", case.tipcodes, case.weights, bad, True, "JC69", 1, case.blens,
+                   case.freqs, case.rates, case.rs, case.ps)
+        _engine(cases.Case("bad", case.tipcodes, case.weights, bad, True, "JC69", 1, case.blens,
+                           case.freqs, case.rates, case.rs, case.ps))
+    eng = _engine(case)
+    with pytest.raises(PhyloHipError):
+        eng.evaluate_batch(np.tile(case.blens, (2, 1)), np.tile(case.model_vec(), (2, 1)))
