@@ -1,0 +1,306 @@
+#!/usr/bin/env python
+"""Benchmark: log-likelihood + full-gradient evaluations per second.
+
+Metric (BASELINE.json): "log-lik+grad evals/sec (HKY+W4, 69 taxa) at 1/2/4/8
+MI355X; HBM-BW fraction".  One *evaluation* = P-matrices + post-order sweep +
+root + pre-order gradient pass + dL/dP accumulation + finalize (loglik,
+dL/dP[C][B][16], dlogL/dblens, /drs, /dps, root-frequency term), outputs left
+in HBM.  One *step* = one batched evaluation of ``--draws`` independent
+parameter points (distinct branch lengths and kappa per draw, pre-generated
+on the device so nothing is cached across steps).
+
+Workloads:
+  fluA (default)  examples/fluA: 69 taxa, 238 patterns, HKY+W4 strict clock at
+                  the README.md:104-108 means.  Multi-GPU = independent draw
+                  batches per rank (weak scaling, no collective: each rank's
+                  evaluations are complete).
+  synthetic       128 taxa x 1M simulated sites GTR+W4 (phylostan_amd/
+                  synthetic.py).  Multi-GPU = patterns sharded over ranks +
+                  one RCCL all-reduce of the output vector per step (strong
+                  scaling of one evaluation).
+
+Launched as ``python bench.py`` (N=1) or under torch.distributed.run with
+one rank per GPU.  Rank 0 prints ONE JSON line.
+"""
+import argparse
+import hashlib
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+PEAK_HBM_GBPS = 8000.0  # MI355X_MICROARCH.md chip table: HBM3E 8.0 TB/s spec
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--workload", choices=["fluA", "synthetic"], default="fluA")
+    ap.add_argument("--draws", type=int, default=None,
+                    help="parameter points per step (default: fluA 512, synthetic 1)")
+    ap.add_argument("--sites", type=int, default=1_000_000, help="synthetic: simulated sites")
+    ap.add_argument("--cpu-seconds", type=float, default=10.0, help="cpu_baseline sample length")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--single-eval", action="store_true",
+                    help="also time unbatched (draws=1) evaluations and report them")
+    ap.add_argument("--wg-budget", type=int, default=0)
+    ap.add_argument("--g-mode", type=int, default=0)
+    ap.add_argument("--lds-budget", type=int, default=0)
+    ap.add_argument("--json-out", default=None)
+    return ap.parse_args()
+
+
+def kernel_source_hash():
+    h = hashlib.sha1()
+    with open(os.path.join(ROOT, "phylostan_amd", "csrc", "phylo_hip.hip"), "rb") as fp:
+        h.update(fp.read())
+    return h.hexdigest()[:12]
+
+
+def fluA_problem():
+    from tests import cases
+    c = cases.fluA_case()
+    return dict(tipcodes=c.tipcodes, weights=c.weights, peel0=c.peel0, rooted=True, model="HKY",
+                C=4, blens=c.blens, freqs=c.freqs, kappa=5.58, rates=c.rates, rs=c.rs, ps=c.ps)
+
+
+def synthetic_problem(sites):
+    from phylostan_amd import synthetic
+    cache = "/tmp/phylostan_amd_synth_%d.npz" % sites
+    if os.path.exists(cache):
+        z = np.load(cache, allow_pickle=False)
+        d = {k: z[k] for k in z.files}
+    else:
+        pd, prm = synthetic.simulate(n_sites=sites)
+        d = dict(tipcodes=pd.tipcodes, weights=pd.weights, peel0=pd.peel0, **prm)
+        try:
+            np.savez(cache + ".tmp.npz", **d)
+            os.replace(cache + ".tmp.npz", cache)
+        except OSError:
+            pass
+    return dict(tipcodes=d["tipcodes"], weights=d["weights"], peel0=d["peel0"], rooted=True,
+                model="GTR", C=4, blens=d["blens"], freqs=d["freqs"], kappa=None, rates=d["rates"],
+                rs=d["rs"], ps=d["ps"])
+
+
+def algorithmic_bytes(S, P, C, nslots, B, draws):
+    """HBM bytes one sweep launch must move (DESIGN.md "Roofline"):
+    every non-root internal partial written once + read once (2 x 32 B per
+    slot per column), tip codes (S B/pattern), weights (8 B/pattern),
+    P-matrices in + dL/dP out (2 x 128 B per branch-category)."""
+    per_draw = 64 * nslots * C * P + S * P + 8 * P + 256 * B * C
+    return per_draw * draws
+
+
+def survey_bytes(S, P, C, draws):
+    """SURVEY.md 8d model: B_eval = P (224 C (S-2) + 3 S + 16)."""
+    return P * (224 * C * (S - 2) + 3 * S + 16) * draws
+
+
+def cpu_baseline(prob, seconds):
+    """The C oracle (oracle/cpu_pruner.c, 'port') on the same workload,
+    single-threaded (Stan evaluates log_prob on one thread per chain)."""
+    from oracle import cpu
+    from phylostan_amd import models
+    kind = models.MODEL_IDS[prob["model"]]
+    mv = models.model_vector(prob["freqs"], prob["rates"], prob["rs"], prob["ps"])
+    S, P = prob["tipcodes"].shape
+    n = 0
+    t0 = time.perf_counter()
+    out = None
+    while True:
+        out, _ = cpu.evaluate(prob["tipcodes"], prob["weights"], prob["peel0"], prob["rooted"], kind, mv,
+                              prob["blens"], prob["C"], nthreads=1)
+        n += 1
+        el = time.perf_counter() - t0
+        if el >= seconds:
+            break
+    return dict(value=n / el, unit="evals/s", cores=1, kind="port",
+                sample="%d full log-lik+grad evaluations of the %d-taxon x %d-pattern workload in %.1f s, "
+                       "1 thread (oracle/cpu_pruner.c, gcc -O2)" % (n, S, P, el)), out
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+
+    from phylostan_amd import models
+    from phylostan_amd.distributed import ShardedLikelihood
+
+    if args.workload == "fluA":
+        prob = fluA_problem()
+        draws = args.draws or 512
+        shard_world, shard_rank = 1, 0  # replicas: every rank runs complete evaluations
+    else:
+        prob = synthetic_problem(args.sites)
+        draws = args.draws or 1
+        shard_world, shard_rank = world, rank
+    S, P = prob["tipcodes"].shape
+    C = prob["C"]
+
+    sl = ShardedLikelihood(prob["tipcodes"], prob["weights"], prob["peel0"], prob["rooted"], prob["model"],
+                           C, shard_rank, shard_world, device=local, max_draws=draws)
+    eng = sl.engine
+    if args.wg_budget or args.g_mode or args.lds_budget:
+        eng.set_tuning(args.wg_budget, args.g_mode, args.lds_budget)
+    info = eng.program_info()
+    info.update(eng.lds_plan())
+    B = eng.B
+    P_local = sl.p1 - sl.p0
+
+    # pre-generated, distinct parameter points for every step (seeded per rank)
+    rng = np.random.default_rng(1234 + rank)
+    nsets = args.warmup + args.steps
+    nuniq = min(nsets, 16)
+    blens = np.empty((nuniq, draws, B))
+    mvs = np.empty((nuniq, draws, 10 + 2 * C))
+    for k in range(nuniq):
+        scale = rng.uniform(0.8, 1.25, (draws, 1))
+        blens[k] = prob["blens"][None, :] * scale
+        for d in range(draws):
+            if prob["kappa"] is not None:
+                rates = models.hky_exchangeabilities(prob["kappa"] * rng.uniform(0.8, 1.25))
+            else:
+                rates = prob["rates"] * rng.uniform(0.9, 1.1, 6)
+            mvs[k, d] = models.model_vector(prob["freqs"], rates, prob["rs"], prob["ps"])
+    d_blens = torch.tensor(blens, device=dev, dtype=torch.float64)
+    d_model = torch.tensor(mvs, device=dev, dtype=torch.float64)
+    d_out = torch.zeros((draws, eng.outlen), device=dev, dtype=torch.float64)
+    stream = torch.cuda.current_stream(dev).cuda_stream
+
+    def step(k):
+        sl.evaluate(d_blens[k % nuniq], d_model[k % nuniq], d_out, stream=stream)
+
+    for k in range(args.warmup):
+        step(k)
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    eng.timing_start()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for k in range(args.steps):
+        step(args.warmup + k)
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    t1 = time.perf_counter()
+    kern_ms, nlaunch = eng.timing_read()
+    elapsed = t1 - t0
+    if world > 1:
+        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+        km = torch.tensor([kern_ms / max(nlaunch, 1)], device=dev, dtype=torch.float64)
+        dist.all_reduce(km, op=dist.ReduceOp.MAX)
+        kern_avg_ms = float(km.item())
+    else:
+        kern_avg_ms = kern_ms / max(nlaunch, 1)
+    ll_last = float(d_out[0, 0].item())
+
+    if args.workload == "fluA":
+        total_evals = world * draws * args.steps
+    else:
+        total_evals = draws * args.steps
+    value = total_evals / elapsed
+
+    single = None
+    if args.single_eval and rank == 0:
+        d_out1 = torch.zeros((1, eng.outlen), device=dev, dtype=torch.float64)
+        for k in range(10):
+            eng.evaluate_device(d_blens[0, :1].data_ptr(), d_model[0, :1].data_ptr(), d_out1.data_ptr(), 0,
+                                n_draws=1, stream=stream)
+        torch.cuda.synchronize(dev)
+        n1 = 200
+        ta = time.perf_counter()
+        for k in range(n1):
+            eng.evaluate_device(d_blens[k % nuniq, :1].data_ptr(), d_model[k % nuniq, :1].data_ptr(),
+                                d_out1.data_ptr(), 0, n_draws=1, stream=stream)
+        torch.cuda.synchronize(dev)
+        tb = time.perf_counter()
+        single = dict(evals_per_s=n1 / (tb - ta), us_per_eval=1e6 * (tb - ta) / n1)
+
+    alg = algorithmic_bytes(S, P_local, C, info["nslots"], B, draws)
+    achieved = alg / (kern_avg_ms * 1e-3) / 1e9
+    traffic = None
+    pmc = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    if os.path.exists(pmc):
+        try:
+            with open(pmc) as fp:
+                rec = json.load(fp)
+            key = "%s:%d" % (args.workload, draws)
+            if rec.get("kernel_source") == kernel_source_hash() and key in rec.get("per_launch_bytes", {}):
+                traffic = rec["per_launch_bytes"][key]
+        except (OSError, ValueError):
+            traffic = None
+
+    cpu = None
+    if rank == 0 and not args.no_cpu_baseline:
+        cpu, cpu_out = cpu_baseline(prob, args.cpu_seconds)
+        # the cpu sample evaluates draw-0's nominal parameters; report its loglik
+        cpu["loglik"] = float(cpu_out[0])
+
+    if rank == 0:
+        rec = {
+            "metric": "log-lik+grad evals/sec (HKY+W4, 69 taxa) at 1/2/4/8 MI355X; HBM-BW fraction"
+            if args.workload == "fluA" else "log-lik+grad evals/sec (GTR+W4, 128 taxa x 1M sites)",
+            "value": value,
+            "unit": "evals/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": 1e3 * elapsed / args.steps,
+            "higher_is_better": True,
+            "scaling": "weak" if args.workload == "fluA" else "strong",
+            "vs_baseline": None,
+            "dtype": "f64",
+            "data": "fluA alignment patterns + input-tree heights (tests/golden fixture of examples/fluA)"
+            if args.workload == "fluA" else "synthetic (Kingman 128 taxa, simulated GTR+W4 sites, seed 0)",
+            "config": {
+                "workload": "fluA HKY+W4 strict clock, %d parameter draws per step" % draws
+                if args.workload == "fluA" else "synthetic 128 x %d sites GTR+W4, pattern-sharded" % args.sites,
+                "taxa": S, "patterns": P, "patterns_per_rank": P_local, "categories": C,
+                "branches": B, "draws_per_step": draws,
+                "parallelism": ("replicas%d" % world) if args.workload == "fluA" else ("patterns%d" % world),
+            },
+            "roofline": {
+                "bound": "hbm", "achieved": achieved, "peak": PEAK_HBM_GBPS, "unit": "GB/s",
+                "frac": achieved / PEAK_HBM_GBPS, "traffic": traffic,
+                "kernel": "sweep_kernel", "kernel_avg_ms": kern_avg_ms,
+                "algorithmic_bytes_per_launch": alg,
+                "survey_model_bytes_per_launch": survey_bytes(S, P_local, C, draws),
+            },
+            "cpu_baseline": cpu,
+            "loglik_draw0": ll_last,
+            "single_eval": single,
+            "program": info,
+            "kernel_source": kernel_source_hash(),
+        }
+        line = json.dumps(rec)
+        print(line, flush=True)
+        if args.json_out:
+            with open(args.json_out, "w") as fp:
+                fp.write(line + "\n")
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -10,7 +10,7 @@ import ctypes
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libphylo_hip.so")
+LIB_PATH = os.environ.get("PHYLO_HIP_LIB") or os.path.join(_HERE, "libphylo_hip.so")
 
 PHY_JC69, PHY_HKY, PHY_GTR = 0, 1, 2
 
@@ -38,7 +38,8 @@ SIGNATURES = {
     "phy_sync": (ctypes.c_int, [ctypes.c_void_p]),
     "phy_timing_start": (ctypes.c_int, [ctypes.c_void_p]),
     "phy_timing_read": (ctypes.c_int, [ctypes.c_void_p, _c_double_p, _c_int_p]),
-    "phy_set_tuning": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_int]),
+    "phy_set_tuning": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int]),
+    "phy_lds_plan": (ctypes.c_int, [ctypes.c_void_p, _c_int_p, _c_int_p, _c_int_p]),
 }
 
 

@@ -49,6 +49,9 @@
 namespace {
 
 constexpr int WAVE = 64;
+#ifndef PHY_ABLATE
+#define PHY_ABLATE 0  // diagnostic builds only: 1 no dL/dP accumulation, 2 no reverse pass, 4 no scratch stores
+#endif
 constexpr int STEP_INTS = 8;  // x, y, bx, by, vslot, pad...
 
 thread_local std::string g_err;
@@ -112,6 +115,33 @@ __device__ __forceinline__ V4 matTvec(const M16& M, const V4& v) {
   return r;
 }
 
+// Same products with the matrix read straight from LDS at the point of use
+// (wave-uniform address: broadcast reads), so no 32-VGPR copy stays live.
+__device__ __forceinline__ V4 matvec_p(const double* __restrict__ M, const V4& v) {
+  const double2 m01 = *reinterpret_cast<const double2*>(M + 0), m23 = *reinterpret_cast<const double2*>(M + 2);
+  const double2 m45 = *reinterpret_cast<const double2*>(M + 4), m67 = *reinterpret_cast<const double2*>(M + 6);
+  const double2 m89 = *reinterpret_cast<const double2*>(M + 8), mab = *reinterpret_cast<const double2*>(M + 10);
+  const double2 mcd = *reinterpret_cast<const double2*>(M + 12), mef = *reinterpret_cast<const double2*>(M + 14);
+  V4 r;
+  r.x = fma(m23.y, v.w, fma(m23.x, v.z, fma(m01.y, v.y, m01.x * v.x)));
+  r.y = fma(m67.y, v.w, fma(m67.x, v.z, fma(m45.y, v.y, m45.x * v.x)));
+  r.z = fma(mab.y, v.w, fma(mab.x, v.z, fma(m89.y, v.y, m89.x * v.x)));
+  r.w = fma(mef.y, v.w, fma(mef.x, v.z, fma(mcd.y, v.y, mcd.x * v.x)));
+  return r;
+}
+__device__ __forceinline__ V4 matTvec_p(const double* __restrict__ M, const V4& v) {
+  const double2 m01 = *reinterpret_cast<const double2*>(M + 0), m23 = *reinterpret_cast<const double2*>(M + 2);
+  const double2 m45 = *reinterpret_cast<const double2*>(M + 4), m67 = *reinterpret_cast<const double2*>(M + 6);
+  const double2 m89 = *reinterpret_cast<const double2*>(M + 8), mab = *reinterpret_cast<const double2*>(M + 10);
+  const double2 mcd = *reinterpret_cast<const double2*>(M + 12), mef = *reinterpret_cast<const double2*>(M + 14);
+  V4 r;
+  r.x = fma(mcd.x, v.w, fma(m89.x, v.z, fma(m45.x, v.y, m01.x * v.x)));
+  r.y = fma(mcd.y, v.w, fma(m89.y, v.z, fma(m45.y, v.y, m01.y * v.x)));
+  r.z = fma(mef.x, v.w, fma(mab.x, v.z, fma(m67.x, v.y, m23.x * v.x)));
+  r.w = fma(mef.y, v.w, fma(mab.y, v.z, fma(m67.y, v.y, m23.y * v.x)));
+  return r;
+}
+
 __device__ __forceinline__ V4 tipvec(unsigned code) {
   return {(double)(code & 1u), (double)((code >> 1) & 1u), (double)((code >> 2) & 1u),
           (double)((code >> 3) & 1u)};
@@ -123,29 +153,50 @@ __device__ __forceinline__ double wave_sum(double v) {
   return v;
 }
 
-// Transpose-reduce of 16 per-lane values over the 64 lanes of a wave.  Each
-// step halves the values a lane carries and exchanges the other half with
-// its partner, so 16 sums cost 17 shuffles instead of 96.  On return lane l
-// holds the full sum of entry e(l) = 8*b5 + 4*b4 + 2*b3 + b2 (bits of l),
+// Cross-lane moves on doubles (two 32-bit halves each).
+template <int CTRL>
+__device__ __forceinline__ double dpp_d(double v) {
+  const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(v), CTRL, 0xF, 0xF, false);
+  const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(v), CTRL, 0xF, 0xF, false);
+  return __hiloint2double(hi, lo);
+}
+// v_permlane32_swap (gfx950): a <- [a_lo | b_lo], b <- [a_hi | b_hi]  (32-lane halves)
+__device__ __forceinline__ void swap32(double& a, double& b) {
+  auto l = __builtin_amdgcn_permlane32_swap(__double2loint(a), __double2loint(b), false, false);
+  auto h = __builtin_amdgcn_permlane32_swap(__double2hiint(a), __double2hiint(b), false, false);
+  a = __hiloint2double(h[0], l[0]);
+  b = __hiloint2double(h[1], l[1]);
+}
+// v_permlane16_swap (gfx950): odd 16-lane rows of a <-> even rows of b
+__device__ __forceinline__ void swap16(double& a, double& b) {
+  auto l = __builtin_amdgcn_permlane16_swap(__double2loint(a), __double2loint(b), false, false);
+  auto h = __builtin_amdgcn_permlane16_swap(__double2hiint(a), __double2hiint(b), false, false);
+  a = __hiloint2double(h[0], l[0]);
+  b = __hiloint2double(h[1], l[1]);
+}
+constexpr int DPP_ROW_ROR8 = 0x128;       // lane l <- l ^ 8 within a 16-lane row
+constexpr int DPP_ROW_HALF_MIRROR = 0x141;  // lane i <- 7 - i within 8 lanes (bit 2 flips)
+constexpr int DPP_QUAD_XOR1 = 0xB1;       // quad_perm [1,0,3,2]
+constexpr int DPP_QUAD_XOR2 = 0x4E;       // quad_perm [2,3,0,1]
+
+// Transpose-reduce of 16 per-lane values over the 64 lanes of a wave, all in
+// VALU cross-lane ops (no LDS, no waitcnt).  Each halving stage pairs lanes
+// that differ in one bit and leaves each lane with the half selected by that
+// bit, summed with its partner's: bit 5 and bit 4 by the gfx950 permlane32/16
+// swaps (no selects needed), bit 3 by DPP row_ror:8, bit 2 by DPP
+// row_half_mirror; two quad DPP adds finish the sums.  On return lane l holds
+// the full sum of entry e(l) = 8*b5 + 4*b4 + 2*b3 + b2 (bits of l),
 // replicated over l&3.  The summation tree is fixed: deterministic.
 __device__ __forceinline__ double reduce16(double (&v)[16], int lane) {
-  {
-    const bool hi = lane & 32;
 #pragma unroll
-    for (int k = 0; k < 8; ++k) {
-      const double send = hi ? v[k] : v[k + 8];
-      const double keep = hi ? v[k + 8] : v[k];
-      v[k] = keep + __shfl_xor(send, 32, WAVE);
-    }
+  for (int k = 0; k < 8; ++k) {  // bit 5: lanes <32 keep entry k, >=32 entry k+8
+    swap32(v[k], v[k + 8]);
+    v[k] += v[k + 8];
   }
-  {
-    const bool hi = lane & 16;
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      const double send = hi ? v[k] : v[k + 4];
-      const double keep = hi ? v[k + 4] : v[k];
-      v[k] = keep + __shfl_xor(send, 16, WAVE);
-    }
+  for (int k = 0; k < 4; ++k) {  // bit 4: even rows keep k, odd rows k+4
+    swap16(v[k], v[k + 4]);
+    v[k] += v[k + 4];
   }
   {
     const bool hi = lane & 8;
@@ -153,18 +204,18 @@ __device__ __forceinline__ double reduce16(double (&v)[16], int lane) {
     for (int k = 0; k < 2; ++k) {
       const double send = hi ? v[k] : v[k + 2];
       const double keep = hi ? v[k + 2] : v[k];
-      v[k] = keep + __shfl_xor(send, 8, WAVE);
+      v[k] = keep + dpp_d<DPP_ROW_ROR8>(send);
     }
   }
   {
     const bool hi = lane & 4;
     const double send = hi ? v[0] : v[1];
     const double keep = hi ? v[1] : v[0];
-    v[0] = keep + __shfl_xor(send, 4, WAVE);
+    v[0] = keep + dpp_d<DPP_ROW_HALF_MIRROR>(send);
   }
   double s = v[0];
-  s += __shfl_xor(s, 2, WAVE);
-  s += __shfl_xor(s, 1, WAVE);
+  s += dpp_d<DPP_QUAD_XOR1>(s);
+  s += dpp_d<DPP_QUAD_XOR2>(s);
   return s;
 }
 
@@ -178,85 +229,204 @@ __device__ __forceinline__ int reduce16_entry(int lane) {
 struct SweepArgs {
   const uint8_t* tips;    // [S][Ppad] state masks
   const double* weights;  // [Ppad]   (0 on padding)
-  const int* prog;        // [nsteps][STEP_INTS]
-  const double* pm;       // [draw][C][B][16]
+  const double* pprog;    // [draw][C][nsteps][2][16]  P of both children, program order
   const double* model;    // [draw][10+2C]
   double2* scratch;       // [wg][nslots][2][C*64]
-  double* gslot;          // [wg][C][B][16]
+  double* gslot;          // [wg][C][nsteps][2][16]  dL/dP partial sums, program order
   double* sslot;          // [wg][C][8]
   double* site_ll;        // [draw][P] or null
-  int S, P, Ppad, C, B, nsteps, nslots, nblk, depth;
+  unsigned long long* stamps;  // diagnostic builds (PHY_STAMP): [wg][C][8] s_memtime
+  int S, P, Ppad, C, nsteps, nslots, nblk, depth, cs;
 };
 
+#ifndef PHY_STAMP
+#define PHY_STAMP 0
+#endif
+#define STAMP(k)                                                                      \
+  do {                                                                                \
+    if (PHY_STAMP && a.stamps && blk0 && lane == 0)                                   \
+      a.stamps[((size_t)wg * C + c) * 8 + (k)] = __builtin_amdgcn_s_memtime();         \
+  } while (0)
+
 // LDS carve (all offsets multiples of 16 B):
-//   stacks  C * depth * 2 * 64 double2
-//   tips    S * 64 bytes (rounded to 16)
-//   rootL   C * 64 double
-//   G       C * B * 16 double            (GLDS only)
-__host__ __device__ inline size_t lds_bytes(int S, int C, int B, int depth, bool glds) {
-  size_t b = (size_t)C * depth * 2 * WAVE * 16;
+//   P chunk  C * cs * 32 double   (both children's matrices of steps [s0, s0+cs))
+//   G chunk  C * cs * 32 double   (dL/dP of the same branches)
+//   stacks   C * depth * 2 * 64 double2
+//   tips     S * 64 bytes (rounded to 16)
+//   rootL    C * 64 double
+__host__ __device__ inline size_t lds_bytes(int S, int C, int depth, int cs) {
+  size_t b = 2 * (size_t)C * cs * 32 * 8;
+  b += (size_t)C * depth * 2 * WAVE * 16;
   b += ((size_t)S * WAVE + 15) / 16 * 16;
   b += (size_t)C * WAVE * 8;
-  if (glds) b += (size_t)C * B * 16 * 8;
   return b;
 }
 
-template <bool GLDS, int MAXT>
-__global__ void __launch_bounds__(MAXT) sweep_kernel(SweepArgs a) {
+// Buffer resource for the workgroup's scratch region (T8): buffer loads
+// past num_records return zeros without touching memory, which lets the
+// reverse pass issue its prefetch unconditionally (tip children get an
+// out-of-range offset) -- no divergent-looking load paths for the waitcnt
+// pass to merge pessimistically.
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* base, uint32_t bytes) {
+  const uint64_t a = reinterpret_cast<uint64_t>(base);
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)a);
+  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(a >> 32));
+  const uint32_t n = __builtin_amdgcn_readfirstlane(bytes);
+  void* p = reinterpret_cast<void*>(((uint64_t)hi << 32) | lo);
+  return __builtin_amdgcn_make_buffer_rsrc(p, (short)0, (int)n, 0x00020000);
+}
+
+// `prog` is a separate __restrict__ const argument so the backend can prove
+// it is never written and read it with scalar (s_load) instructions; inside
+// the struct it would be read with vector loads + a full vmcnt(0) per step.
+template <int MAXT>
+__global__ void __launch_bounds__(MAXT) sweep_kernel(SweepArgs a, const int* __restrict__ prog) {
   extern __shared__ __attribute__((aligned(16))) unsigned char lds_raw[];
   const int lane = threadIdx.x & (WAVE - 1);
   const int c = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int nthreads = blockDim.x;
   const int draw = blockIdx.y;
   const int wg = blockIdx.y * gridDim.x + blockIdx.x;
-  const int C = a.C, B = a.B;
+  const int C = a.C, cs = a.cs, nsteps = a.nsteps;
   const int ncolwg = C * WAVE;
+  const bool one_chunk = cs >= nsteps;
+  bool blk0 = true;  // first pattern block of this workgroup (diagnostic stamps)
+  if (PHY_STAMP && a.stamps && lane == 0) {
+    a.stamps[((size_t)wg * C + c) * 8 + 6] = __builtin_amdgcn_s_memrealtime();
+    a.stamps[((size_t)wg * C + c) * 8 + 0] = __builtin_amdgcn_s_memtime();
+  }
 
-  double2* stk = reinterpret_cast<double2*>(lds_raw) + (size_t)c * a.depth * 2 * WAVE;
-  unsigned char* tipl = lds_raw + (size_t)C * a.depth * 2 * WAVE * 16;
+  double* pl = reinterpret_cast<double*>(lds_raw);  // [C][cs][2][16]
+  double* gl = pl + (size_t)C * cs * 32;             // [C][cs][2][16]
+  double2* stk = reinterpret_cast<double2*>(gl + (size_t)C * cs * 32) + (size_t)c * a.depth * 2 * WAVE;
+  unsigned char* tipl = reinterpret_cast<unsigned char*>(gl + (size_t)C * cs * 32) +
+                        (size_t)C * a.depth * 2 * WAVE * 16;
   double* rootL = reinterpret_cast<double*>(tipl + ((size_t)a.S * WAVE + 15) / 16 * 16);
-  double* gl = rootL + (size_t)C * WAVE;  // GLDS: [C][B][16]
 
   const double* mdl = a.model + (size_t)draw * (10 + 2 * C);
   const V4 pi = {mdl[0], mdl[1], mdl[2], mdl[3]};
   const double ps_c = mdl[10 + C + c];
-  const double* pmc = a.pm + ((size_t)draw * C + c) * B * 16;
+  const double* pprog_d = a.pprog + (size_t)draw * C * nsteps * 32;
   double2* scr = a.scratch + (size_t)wg * a.nslots * 2 * ncolwg;
-  double* gslot_c = a.gslot + ((size_t)wg * C + c) * B * 16;
+  double* gslot_wg = a.gslot + (size_t)wg * C * nsteps * 32;
+  const uint32_t scr_bytes = (uint32_t)((size_t)a.nslots * 2 * ncolwg * 16);
+  const __amdgpu_buffer_rsrc_t srd = make_rsrc(scr, scr_bytes);
 
   const int e = reduce16_entry(lane);
   const bool gowner = (lane & 3) == 0;
-  if (GLDS) {
-    for (int k = threadIdx.x; k < C * B * 16; k += nthreads) gl[k] = 0.0;
-  } else if (gowner) {
-    for (int b = 0; b < B; ++b) gslot_c[b * 16 + e] = 0.0;
-  }
+
+  for (int k = threadIdx.x; k < C * cs * 32; k += nthreads) gl[k] = 0.0;
 
   double acc_ll = 0.0, acc_dps = 0.0;
   V4 acc_f = {0.0, 0.0, 0.0, 0.0};
 
-  auto push = [&](int& sp, const V4& v) {
-    stk[(sp * 2 + 0) * WAVE + lane] = make_double2(v.x, v.y);
-    stk[(sp * 2 + 1) * WAVE + lane] = make_double2(v.z, v.w);
-    ++sp;
+  // P-matrices (and the matching dL/dP accumulators) live in LDS, in chunks
+  // of cs program steps; one chunk = the whole program when it fits, staged
+  // once per workgroup.  Reads use wave-uniform LDS addresses (broadcast).
+  int chunk_lo = -1;
+  // Hand the LDS G chunk to this workgroup's global slot and zero it: a
+  // plain store the first time the slot region is written (the workgroup's
+  // first pattern block), otherwise load-add-store with 8 loads in flight
+  // per thread.
+  bool g_first = true;
+  auto flush_g = [&]() {
+    if (chunk_lo < 0) return;
+    const int n = min(cs, nsteps - chunk_lo);
+    const int q = n * 32;  // doubles per category
+    for (int cc = 0; cc < C; ++cc) {
+      double* gp = gslot_wg + ((size_t)cc * nsteps + chunk_lo) * 32;
+      double* lp = gl + (size_t)cc * cs * 32;
+      for (int k0 = threadIdx.x; k0 < q; k0 += nthreads * 8) {
+        double old[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          const int k = k0 + u * nthreads;
+          old[u] = (!g_first && k < q) ? gp[k] : 0.0;
+        }
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          const int k = k0 + u * nthreads;
+          if (k < q) {
+            gp[k] = old[u] + lp[k];
+            lp[k] = 0.0;
+          }
+        }
+      }
+    }
   };
-  auto pop = [&](int& sp) -> V4 {
+  auto ensure_chunk = [&](int s, bool reverse) {
+    const int lo = (s / cs) * cs;
+    if (lo == chunk_lo) return;  // workgroup-uniform
+    __syncthreads();
+    if (reverse) flush_g();
+    // per category the chunk is one contiguous run of n*32 doubles; 8 loads
+    // in flight per thread before the LDS writes (a load->write loop would
+    // serialise one memory round trip per element)
+    const int n = min(cs, nsteps - lo);
+    const int q2 = n * 16;  // double2 per category
+    for (int cc = 0; cc < C; ++cc) {
+      const double2* src = reinterpret_cast<const double2*>(pprog_d + ((size_t)cc * nsteps + lo) * 32);
+      double2* dst = reinterpret_cast<double2*>(pl + (size_t)cc * cs * 32);
+      for (int k0 = threadIdx.x; k0 < q2; k0 += nthreads * 8) {
+        double2 buf[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          const int k = k0 + u * nthreads;
+          buf[u] = (k < q2) ? src[k] : make_double2(0.0, 0.0);
+        }
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          const int k = k0 + u * nthreads;
+          if (k < q2) dst[k] = buf[u];
+        }
+      }
+    }
+    __syncthreads();
+    chunk_lo = lo;
+  };
+  auto pmat = [&](int s, int which) -> const double* {
+    return pl + ((size_t)c * cs + (s - chunk_lo)) * 32 + which * 16;
+  };
+
+  // Pending-vector stack: the most recent entry stays in registers (most
+  // pushes are popped by the very next step), older ones live in LDS.
+  int sp = 0;
+  bool has_top = false;
+  double t0 = 0.0, t1 = 0.0, t2 = 0.0, t3 = 0.0;  // top of stack (scalars: keeps it in VGPRs)
+  auto push = [&](V4 v) {
+    if (has_top) {
+      stk[(sp * 2 + 0) * WAVE + lane] = make_double2(t0, t1);
+      stk[(sp * 2 + 1) * WAVE + lane] = make_double2(t2, t3);
+      ++sp;
+    }
+    t0 = v.x;
+    t1 = v.y;
+    t2 = v.z;
+    t3 = v.w;
+    has_top = true;
+  };
+  auto pop = [&]() -> V4 {
+    if (has_top) {
+      has_top = false;
+      return {t0, t1, t2, t3};
+    }
     --sp;
     const double2 lo = stk[(sp * 2 + 0) * WAVE + lane];
     const double2 hi = stk[(sp * 2 + 1) * WAVE + lane];
     return {lo.x, lo.y, hi.x, hi.y};
   };
-  auto gacc = [&](int b, const V4& r, const V4& p) {
+  // dL/dP_{branch of (s, which)} += r (x) p, reduced over the wave; the lane
+  // owning entry e adds it to the LDS G chunk (one lane per address)
+  auto gacc = [&](int s, int which, const V4& r, const V4& p) {
     double v[16] = {r.x * p.x, r.x * p.y, r.x * p.z, r.x * p.w, r.y * p.x, r.y * p.y,
                     r.y * p.z, r.y * p.w, r.z * p.x, r.z * p.y, r.z * p.z, r.z * p.w,
                     r.w * p.x, r.w * p.y, r.w * p.z, r.w * p.w};
-    const double s = reduce16(v, lane);
-    if (gowner) {
-      if (GLDS)
-        gl[((size_t)c * B + b) * 16 + e] += s;
-      else
-        gslot_c[b * 16 + e] += s;
+    if (PHY_ABLATE & 1) {
+      asm volatile("" ::"v"(v[0]), "v"(v[5]), "v"(v[10]), "v"(v[15]));
+      return;
     }
+    const double sum = reduce16(v, lane);
+    if (gowner) gl[((size_t)c * cs + (s - chunk_lo)) * 32 + which * 16 + e] += sum;
   };
 
   for (int blk = blockIdx.x; blk < a.nblk; blk += gridDim.x) {
@@ -267,43 +437,50 @@ __global__ void __launch_bounds__(MAXT) sweep_kernel(SweepArgs a) {
       const uint32_t* src = reinterpret_cast<const uint32_t*>(a.tips);
       uint32_t* dst = reinterpret_cast<uint32_t*>(tipl);
       const int rowq = a.Ppad / 4;
-      for (int k = threadIdx.x; k < a.S * (WAVE / 4); k += nthreads) {
-        const int t = k >> 4, q = k & 15;
-        dst[k] = src[(size_t)t * rowq + blk * (WAVE / 4) + q];
+      const int nq = a.S * (WAVE / 4);
+      for (int k0 = threadIdx.x; k0 < nq; k0 += nthreads * 8) {
+        uint32_t buf[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          const int k = k0 + u * nthreads;
+          buf[u] = (k < nq) ? src[(size_t)(k >> 4) * rowq + blk * (WAVE / 4) + (k & 15)] : 0u;
+        }
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          const int k = k0 + u * nthreads;
+          if (k < nq) dst[k] = buf[u];
+        }
       }
     }
     __syncthreads();
 
+    STAMP(1);
     // ------------------------------ forward ------------------------------
-    int sp = 0;
+    sp = 0;
+    has_top = false;
     V4 proot = {0, 0, 0, 0};
-    for (int s = 0; s < a.nsteps; ++s) {
-      const int* st = a.prog + s * STEP_INTS;
-      const int x = st[0], y = st[1], bx = st[2], by = st[3], vs = st[4];
-      V4 ay, ax;
-      if (y >= 0) {
-        ay = tipvec(tipl[y * WAVE + lane]);
-      } else {
-        ay = pop(sp);
-      }
-      if (by >= 0) ay = matvec(load_m(pmc + (size_t)by * 16), ay);
-      if (x >= 0) {
-        ax = tipvec(tipl[x * WAVE + lane]);
-      } else {
-        ax = pop(sp);
-      }
-      if (bx >= 0) ax = matvec(load_m(pmc + (size_t)bx * 16), ax);
+    for (int s = 0; s < nsteps; ++s) {
+      ensure_chunk(s, false);
+      const int* st = prog + s * STEP_INTS;
+      const int x = st[0], y = st[1], vs = st[4];
+      const V4 cy = (y >= 0) ? tipvec(tipl[y * WAVE + lane]) : pop();
+      const V4 ay = matvec_p(pmat(s, 1), cy);  // identity for a merged branch
+      const V4 cx = (x >= 0) ? tipvec(tipl[x * WAVE + lane]) : pop();
+      const V4 ax = matvec_p(pmat(s, 0), cx);
       const V4 pv = vmul(ax, ay);
       if (vs >= 0) {
-        double2* dst = scr + (size_t)vs * 2 * ncolwg + c * WAVE + lane;
-        dst[0] = make_double2(pv.x, pv.y);
-        dst[ncolwg] = make_double2(pv.z, pv.w);
-        push(sp, pv);
+        if (!(PHY_ABLATE & 4)) {
+          double2* dst = scr + (size_t)vs * 2 * ncolwg + c * WAVE + lane;
+          dst[0] = make_double2(pv.x, pv.y);
+          dst[ncolwg] = make_double2(pv.z, pv.w);
+        }
+        push(pv);
       } else {
         proot = pv;
       }
     }
 
+    STAMP(2);
     // ------------------------- root / site log L -------------------------
     const double fp = vdot(pi, proot);  // pi . p_root,c
     rootL[c * WAVE + lane] = ps_c * fp;
@@ -325,38 +502,67 @@ __global__ void __launch_bounds__(MAXT) sweep_kernel(SweepArgs a) {
     acc_f.z = fma(s_c, proot.z, acc_f.z);
     acc_f.w = fma(s_c, proot.w, acc_f.w);
 
+    STAMP(3);
     // ------------------------------ reverse ------------------------------
+    // Software-pipelined one step deep: the children of step s-1 are
+    // requested before step s is computed.  Scratch partials come through
+    // the buffer descriptor; a tip child gets an out-of-range offset (the
+    // load returns 0 and moves no data) and its code is read from LDS.
     sp = 0;
-    for (int s = a.nsteps - 1; s >= 0; --s) {
-      const int* st = a.prog + s * STEP_INTS;
-      const int x = st[0], y = st[1], bx = st[2], by = st[3];
-      const V4 qv = (s == a.nsteps - 1) ? pi : pop(sp);
-      V4 px, py;
-      if (x >= 0) {
-        px = tipvec(tipl[x * WAVE + lane]);
-      } else {
-        const double2* src = scr + (size_t)(-x - 1) * 2 * ncolwg + c * WAVE + lane;
-        const double2 lo = src[0], hi = src[ncolwg];
-        px = {lo.x, lo.y, hi.x, hi.y};
+    has_top = false;
+    const uint32_t col_off = (uint32_t)((c * WAVE + lane) * 16);
+    auto ld_off = [&](int code) -> uint32_t {
+      return code < 0 ? (uint32_t)((-code - 1) * 2 * ncolwg) * 16u + col_off : scr_bytes;
+    };
+    auto ld_partial = [&](uint32_t off) -> V4 {
+      const auto lo = __builtin_amdgcn_raw_buffer_load_b128(srd, off, 0, 0);
+      const auto hi = __builtin_amdgcn_raw_buffer_load_b128(srd, off + (uint32_t)ncolwg * 16u, 0, 0);
+      V4 r;
+      r.x = __hiloint2double((int)lo[1], (int)lo[0]);
+      r.y = __hiloint2double((int)lo[3], (int)lo[2]);
+      r.z = __hiloint2double((int)hi[1], (int)hi[0]);
+      r.w = __hiloint2double((int)hi[3], (int)hi[2]);
+      return r;
+    };
+    if (!(PHY_ABLATE & 2)) {
+      const int* st = prog + (nsteps - 1) * STEP_INTS;
+      int x = st[0], y = st[1];
+      V4 lx = ld_partial(ld_off(x)), ly = ld_partial(ld_off(y));
+      unsigned tx = tipl[max(x, 0) * WAVE + lane], ty = tipl[max(y, 0) * WAVE + lane];
+      for (int s = nsteps - 1; s >= 0; --s) {
+        ensure_chunk(s, true);
+        const int* sn = prog + max(s - 1, 0) * STEP_INTS;
+        const int nx = sn[0], ny = sn[1];
+        const V4 nlx = ld_partial(ld_off(nx)), nly = ld_partial(ld_off(ny));
+        const unsigned ntx = tipl[max(nx, 0) * WAVE + lane], nty = tipl[max(ny, 0) * WAVE + lane];
+        const int* sc_ = prog + s * STEP_INTS;
+        const int bx = sc_[2], by = sc_[3];
+        const V4 px = (x >= 0) ? tipvec(tx) : lx;
+        const V4 py = (y >= 0) ? tipvec(ty) : ly;
+        const V4 qv = (s == nsteps - 1) ? pi : pop();
+        const V4 ax = matvec_p(pmat(s, 0), px);
+        const V4 rx = vmul(qv, matvec_p(pmat(s, 1), py));
+        const V4 ry = vmul(qv, ax);
+        if (x < 0) push(matTvec_p(pmat(s, 0), rx));
+        if (y < 0) push(matTvec_p(pmat(s, 1), ry));
+        if (bx >= 0) gacc(s, 0, vscale(rx, s_c), px);
+        if (by >= 0) gacc(s, 1, vscale(ry, s_c), py);
+        x = nx;
+        y = ny;
+        lx = nlx;
+        ly = nly;
+        tx = ntx;
+        ty = nty;
       }
-      if (y >= 0) {
-        py = tipvec(tipl[y * WAVE + lane]);
-      } else {
-        const double2* src = scr + (size_t)(-y - 1) * 2 * ncolwg + c * WAVE + lane;
-        const double2 lo = src[0], hi = src[ncolwg];
-        py = {lo.x, lo.y, hi.x, hi.y};
+      if (!one_chunk) {  // hand the last chunk's sums to the slot
+        __syncthreads();
+        flush_g();
+        __syncthreads();
+        g_first = false;  // every chunk of the slot has now been written once
       }
-      // Matrices are re-read (scalar loads, K$ hits) rather than kept live
-      // across the step: two live 4x4 fp64 matrices cost 64 SGPRs.
-      const V4 ax = (bx >= 0) ? matvec(load_m(pmc + (size_t)bx * 16), px) : px;
-      const V4 ay = (by >= 0) ? matvec(load_m(pmc + (size_t)by * 16), py) : py;
-      const V4 rx = vmul(qv, ay);
-      const V4 ry = vmul(qv, ax);
-      if (bx >= 0) gacc(bx, vscale(rx, s_c), px);
-      if (x < 0) push(sp, bx >= 0 ? matTvec(load_m(pmc + (size_t)bx * 16), rx) : rx);
-      if (by >= 0) gacc(by, vscale(ry, s_c), py);
-      if (y < 0) push(sp, by >= 0 ? matTvec(load_m(pmc + (size_t)by * 16), ry) : ry);
     }
+    STAMP(4);
+    blk0 = false;
     __syncthreads();  // tips / rootL are rewritten by the next block
   }
 
@@ -376,10 +582,13 @@ __global__ void __launch_bounds__(MAXT) sweep_kernel(SweepArgs a) {
     ss[4] = acc_f.z;
     ss[5] = acc_f.w;
   }
-  if (GLDS) {
+  if (one_chunk) {  // G accumulated in LDS for the workgroup's lifetime
     __syncthreads();
-    double* dst = a.gslot + (size_t)wg * C * B * 16;
-    for (int k = threadIdx.x; k < C * B * 16; k += nthreads) dst[k] = gl[k];
+    flush_g();
+  }
+  if (PHY_STAMP && a.stamps && lane == 0) {
+    a.stamps[((size_t)wg * C + c) * 8 + 5] = __builtin_amdgcn_s_memtime();
+    a.stamps[((size_t)wg * C + c) * 8 + 7] = __builtin_amdgcn_s_memrealtime();
   }
 }
 
@@ -389,9 +598,10 @@ __global__ void __launch_bounds__(MAXT) sweep_kernel(SweepArgs a) {
 struct PmatArgs {
   const double* model;  // [draw][10+2C]
   const double* blens;  // [draw][B]
-  double* pm;           // [draw][C][B][16]
-  double* qp;           // [draw][C][B][16]  Q P  (= dP/dt)
-  int C, B, kind;
+  const int* gpos;      // [B] program position (step*2 + which) of branch b
+  double* pprog;        // [draw][C][nsteps][2][16]  program order (identity if merged)
+  double* qp;           // [draw][C][B][16]  Q P  (= dP/dt), branch order
+  int C, B, kind, nsteps, merged_pos;
 };
 
 // Cyclic Jacobi eigendecomposition of a symmetric 4x4 (A overwritten).
@@ -435,13 +645,27 @@ __device__ void jacobi4(double A[4][4], double V[4][4], double lam[4]) {
   for (int i = 0; i < 4; ++i) lam[i] = A[i][i];
 }
 
+constexpr int PM_ITEMS = 4;  // (category, branch) items per thread per round
+
 __global__ void __launch_bounds__(256) pmat_kernel(PmatArgs a) {
   __shared__ double m1[16], m2[16], lam[4], Q[16];
   const int draw = blockIdx.x;
-  const int C = a.C, B = a.B;
+  const int C = a.C, B = a.B, nsteps = a.nsteps;
   const double* mdl = a.model + (size_t)draw * (10 + 2 * C);
   const double* rs = mdl + 10;
   const double* bl = a.blens + (size_t)draw * B;
+  const int nitem = C * B;
+  // this thread's first round of items: branch times and program positions
+  // are requested before the eigendecomposition so their latency overlaps it
+  double tv[PM_ITEMS];
+  int pos[PM_ITEMS];
+#pragma unroll
+  for (int u = 0; u < PM_ITEMS; ++u) {
+    const int idx = threadIdx.x + u * blockDim.x;
+    const int c = idx / B, b = idx - c * B;
+    tv[u] = (idx < nitem) ? bl[b] * rs[c] : 0.0;
+    pos[u] = (idx < nitem) ? a.gpos[b] : 0;
+  }
   if (threadIdx.x == 0) {
     if (a.kind == PHY_JC69) {
       for (int j = 0; j < 4; ++j)
@@ -466,9 +690,10 @@ __global__ void __launch_bounds__(256) pmat_kernel(PmatArgs a) {
       }
       double A[4][4], V[4][4], l[4], sq[4];
       for (int j = 0; j < 4; ++j) sq[j] = sqrt(f[j]);
+      const double inv_s = 1.0 / s;
       for (int j = 0; j < 4; ++j)
         for (int k = 0; k < 4; ++k) {
-          q[j][k] /= s;  // :868
+          q[j][k] *= inv_s;  // :868
           Q[j * 4 + k] = q[j][k];
         }
       for (int j = 0; j < 4; ++j)  // A = Pi^1/2 Q Pi^-1/2, symmetrised (:870)
@@ -483,35 +708,54 @@ __global__ void __launch_bounds__(256) pmat_kernel(PmatArgs a) {
         }
       }
     }
+    if (a.merged_pos >= 0)  // unrooted: the merged root branch (generate_script.py:1019)
+      for (int c = 0; c < C; ++c) {
+        double* po = a.pprog + (((size_t)draw * C + c) * nsteps * 2 + a.merged_pos) * 16;
+        for (int k = 0; k < 16; ++k) po[k] = (k % 5 == 0) ? 1.0 : 0.0;
+      }
   }
   __syncthreads();
-  for (int idx = threadIdx.x; idx < C * B; idx += blockDim.x) {
-    const int c = idx / B, b = idx - c * B;
-    const double t = bl[b] * rs[c];
-    double P[16];
-    if (a.kind == PHY_JC69) {  // generate_script.py:765-769
-      const double ex = exp(-t / 0.75);
-      const double off = 0.25 - 0.25 * ex, d = 0.25 + 0.75 * ex;
-      for (int k = 0; k < 16; ++k) P[k] = (k % 5 == 0) ? d : off;
-    } else {  // m1 diag(exp(lam t)) m2   (:880)
-      double E[4];
-      for (int l = 0; l < 4; ++l) E[l] = exp(lam[l] * t);
+  for (int base = 0; base < nitem; base += PM_ITEMS * blockDim.x) {
+    if (base > 0) {
+#pragma unroll
+      for (int u = 0; u < PM_ITEMS; ++u) {
+        const int idx = base + threadIdx.x + u * blockDim.x;
+        const int c = idx / B, b = idx - c * B;
+        tv[u] = (idx < nitem) ? bl[b] * rs[c] : 0.0;
+        pos[u] = (idx < nitem) ? a.gpos[b] : 0;
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < PM_ITEMS; ++u) {
+      const int idx = base + threadIdx.x + u * blockDim.x;
+      if (idx >= nitem) break;
+      const int c = idx / B, b = idx - c * B;
+      const double t = tv[u];
+      double P[16];
+      if (a.kind == PHY_JC69) {  // generate_script.py:765-769
+        const double ex = exp(-t / 0.75);
+        const double off = 0.25 - 0.25 * ex, d = 0.25 + 0.75 * ex;
+        for (int k = 0; k < 16; ++k) P[k] = (k % 5 == 0) ? d : off;
+      } else {  // m1 diag(exp(lam t)) m2   (:880)
+        double E[4];
+        for (int l = 0; l < 4; ++l) E[l] = exp(lam[l] * t);
+        for (int j = 0; j < 4; ++j)
+          for (int k = 0; k < 4; ++k) {
+            double acc = 0.0;
+            for (int l = 0; l < 4; ++l) acc = fma(m1[j * 4 + l] * E[l], m2[l * 4 + k], acc);
+            P[j * 4 + k] = acc;
+          }
+      }
+      double* po = a.pprog + (((size_t)draw * C + c) * nsteps * 2 + pos[u]) * 16;
+      double* qo = a.qp + (((size_t)draw * C + c) * B + b) * 16;
+      for (int k = 0; k < 16; ++k) po[k] = P[k];
       for (int j = 0; j < 4; ++j)
         for (int k = 0; k < 4; ++k) {
           double acc = 0.0;
-          for (int l = 0; l < 4; ++l) acc = fma(m1[j * 4 + l] * E[l], m2[l * 4 + k], acc);
-          P[j * 4 + k] = acc;
+          for (int l = 0; l < 4; ++l) acc = fma(Q[j * 4 + l], P[l * 4 + k], acc);
+          qo[j * 4 + k] = acc;
         }
     }
-    double* po = a.pm + (((size_t)draw * C + c) * B + b) * 16;
-    double* qo = a.qp + (((size_t)draw * C + c) * B + b) * 16;
-    for (int k = 0; k < 16; ++k) po[k] = P[k];
-    for (int j = 0; j < 4; ++j)
-      for (int k = 0; k < 4; ++k) {
-        double acc = 0.0;
-        for (int l = 0; l < 4; ++l) acc = fma(Q[j * 4 + l], P[l * 4 + k], acc);
-        qo[j * 4 + k] = acc;
-      }
   }
 }
 
@@ -519,56 +763,112 @@ __global__ void __launch_bounds__(256) pmat_kernel(PmatArgs a) {
 // finalize: fixed-order sums of the per-workgroup slots + chain rule dP/dt
 // ---------------------------------------------------------------------------
 struct FinArgs {
-  const double* gslot;  // [wg][C][B][16]
+  const double* gslot;  // [wg][C][nsteps][2][16]  program order
   const double* sslot;  // [wg][C][8]
   const double* qp;     // [draw][C][B][16]
   const double* blens;  // [draw][B]
   const double* model;  // [draw][10+2C]
+  const int* gpos;      // [B] step*2 + which of branch b
   double* out;          // [draw][outlen]
-  int C, B, gx, outlen;
+  int C, B, nsteps, gx, outlen;
 };
 
-__global__ void __launch_bounds__(256) finalize_kernel(FinArgs a) {
-  extern __shared__ double inner[];  // [C][B]
+// dL/dP: out[draw][og + (c*B + b)*16 + k] = sum over the draw's workgroup
+// slots, in slot order (bitwise deterministic).  64 entries x 4 slot
+// strides per workgroup, 8 loads in flight per thread.
+__global__ void __launch_bounds__(256) finalize_g_kernel(FinArgs a) {
+  __shared__ double part[4][64];
+  const int draw = blockIdx.y;
+  const int C = a.C, B = a.B;
+  const int ng = C * B * 16;
+  const int idx = blockIdx.x * 64 + (threadIdx.x & 63);
+  const int grp = threadIdx.x >> 6;
+  const size_t per_wg = (size_t)C * a.nsteps * 32;
+  const size_t wg0 = (size_t)draw * a.gx;
+  double acc = 0.0;
+  if (idx < ng) {
+    const int c = idx / (B * 16), rem = idx - c * B * 16;
+    const int b = rem >> 4, k = rem & 15;
+    const double* src = a.gslot + wg0 * per_wg + ((size_t)c * a.nsteps * 2 + a.gpos[b]) * 16 + k;
+    for (int w0 = grp; w0 < a.gx; w0 += 4 * 8) {
+      double v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int w = w0 + 4 * u;
+        v[u] = (w < a.gx) ? src[(size_t)w * per_wg] : 0.0;
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u) acc += v[u];
+    }
+  }
+  part[grp][threadIdx.x & 63] = acc;
+  __syncthreads();
+  if (grp == 0 && idx < ng) {
+    const double s = ((part[0][threadIdx.x] + part[1][threadIdx.x]) + part[2][threadIdx.x]) + part[3][threadIdx.x];
+    a.out[(size_t)draw * a.outlen + 1 + B + 2 * C + 4 + idx] = s;
+  }
+}
+
+// Scalars and the chain rule dP/dt = Q P: one workgroup per draw.
+__global__ void __launch_bounds__(256) finalize_s_kernel(FinArgs a) {
+  extern __shared__ double fsh[];  // inner[C*B], bl[B], red[256]
   const int draw = blockIdx.x;
   const int C = a.C, B = a.B;
+  double* inner = fsh;
+  double* bls = fsh + (size_t)C * B;
+  double* red = bls + B;
   double* out = a.out + (size_t)draw * a.outlen;
   const size_t wg0 = (size_t)draw * a.gx;
   const int og = 1 + B + 2 * C + 4;
-  const int ng = C * B * 16;
-  for (int idx = threadIdx.x; idx < ng; idx += blockDim.x) {
-    double s = 0.0;
-    for (int w = 0; w < a.gx; ++w) s += a.gslot[(wg0 + w) * ng + idx];
-    out[og + idx] = s;
+  const double* bl = a.blens + (size_t)draw * B;
+  for (int b = threadIdx.x; b < B; b += blockDim.x) bls[b] = bl[b];
+  // scalar partials: q = 0 ll (category 0 slot), 1..C dps_c, C+1..C+4 dfreq_j
+  for (int q = 0; q < 1 + C + 4; ++q) {
+    double acc = 0.0;
+    for (int w = threadIdx.x; w < a.gx; w += blockDim.x) {
+      const double* ss = a.sslot + (wg0 + w) * C * 8;
+      if (q == 0) {
+        acc += ss[0];
+      } else if (q <= C) {
+        acc += ss[(q - 1) * 8 + 1];
+      } else {
+        double t = 0.0;
+        for (int c = 0; c < C; ++c) t += ss[c * 8 + 2 + (q - 1 - C)];
+        acc += t;
+      }
+    }
+    red[threadIdx.x] = acc;
+    __syncthreads();
+    for (int h = blockDim.x / 2; h > 0; h >>= 1) {
+      if ((int)threadIdx.x < h) red[threadIdx.x] += red[threadIdx.x + h];
+      __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+      const double v = red[0];
+      if (q == 0)
+        out[0] = isfinite(v) ? v : -INFINITY;
+      else if (q <= C)
+        out[1 + B + C + (q - 1)] = v;
+      else
+        out[1 + B + 2 * C + (q - 1 - C)] = v;
+    }
+    __syncthreads();
   }
-  if (threadIdx.x == 0) {
-    double ll = 0.0;
-    for (int w = 0; w < a.gx; ++w) ll += a.sslot[((wg0 + w) * C + 0) * 8 + 0];
-    out[0] = isfinite(ll) ? ll : -INFINITY;
-  }
-  if (threadIdx.x < C) {
-    const int c = threadIdx.x;
-    double d = 0.0;
-    for (int w = 0; w < a.gx; ++w) d += a.sslot[((wg0 + w) * C + c) * 8 + 1];
-    out[1 + B + C + c] = d;
-  }
-  if (threadIdx.x >= 64 && threadIdx.x < 68) {
-    const int j = threadIdx.x - 64;
-    double d = 0.0;
-    for (int w = 0; w < a.gx; ++w)
-      for (int c = 0; c < C; ++c) d += a.sslot[((wg0 + w) * C + c) * 8 + 2 + j];
-    out[1 + B + 2 * C + j] = d;
-  }
-  __syncthreads();
   const double* qp = a.qp + (size_t)draw * C * B * 16;
   for (int idx = threadIdx.x; idx < C * B; idx += blockDim.x) {
+    double g[16], m[16];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+      g[k] = out[og + (size_t)idx * 16 + k];
+      m[k] = qp[(size_t)idx * 16 + k];
+    }
     double s = 0.0;
-    for (int k = 0; k < 16; ++k) s = fma(out[og + (size_t)idx * 16 + k], qp[(size_t)idx * 16 + k], s);
+#pragma unroll
+    for (int k = 0; k < 16; ++k) s = fma(g[k], m[k], s);
     inner[idx] = s;  // dlogL / dt_{b,c}
   }
   __syncthreads();
   const double* rs = a.model + (size_t)draw * (10 + 2 * C) + 10;
-  const double* bl = a.blens + (size_t)draw * B;
   for (int b = threadIdx.x; b < B; b += blockDim.x) {
     double s = 0.0;
     for (int c = 0; c < C; ++c) s = fma(rs[c], inner[c * B + b], s);
@@ -576,7 +876,7 @@ __global__ void __launch_bounds__(256) finalize_kernel(FinArgs a) {
   }
   for (int c = threadIdx.x; c < C; c += blockDim.x) {
     double s = 0.0;
-    for (int b = 0; b < B; ++b) s = fma(bl[b], inner[c * B + b], s);
+    for (int b = 0; b < B; ++b) s = fma(bls[b], inner[c * B + b], s);
     out[1 + B + c] = s;
   }
 }
@@ -589,12 +889,13 @@ __global__ void __launch_bounds__(256) finalize_kernel(FinArgs a) {
 struct phy_ctx {
   int S, P, Ppad, C, B, rooted, kind, max_draws, device;
   int nsteps, nslots, depth, nblk;
-  int wg_budget, g_mode, wg_cap;
+  int wg_budget, g_mode, wg_cap, lds_budget, merged_pos;
   hipStream_t stream;
   uint8_t* d_tips = nullptr;
   double* d_w = nullptr;
   int* d_prog = nullptr;
-  double* d_pm = nullptr;
+  int* d_gpos = nullptr;
+  double* d_pprog = nullptr;
   double* d_qp = nullptr;
   double* d_model = nullptr;
   double* d_blens = nullptr;
@@ -603,6 +904,7 @@ struct phy_ctx {
   double2* d_scratch = nullptr;
   double* d_gslot = nullptr;
   double* d_sslot = nullptr;
+  unsigned long long* d_stamps = nullptr;
   bool timing = false;
   std::vector<hipEvent_t> ev;  // pairs
   int ev_used = 0;
@@ -618,7 +920,7 @@ void free_ctx(phy_ctx* c) {
   int dev_old = 0;
   (void)hipGetDevice(&dev_old);
   (void)hipSetDevice(c->device);
-  void* ptrs[] = {c->d_tips, c->d_w, c->d_prog, c->d_pm, c->d_qp, c->d_model, c->d_blens,
+  void* ptrs[] = {c->d_stamps, c->d_tips, c->d_w, c->d_prog, c->d_gpos, c->d_pprog, c->d_qp, c->d_model, c->d_blens,
                   c->d_out, c->d_site, c->d_scratch, c->d_gslot, c->d_sslot};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
@@ -760,28 +1062,41 @@ int dalloc(T** p, size_t n) {
   return PHY_OK;
 }
 
-bool use_glds(const phy_ctx* c) {
-  if (c->g_mode == 1) return true;
-  if (c->g_mode == 2) return false;
-  return lds_bytes(c->S, c->C, c->B, c->depth, true) <= (size_t)c->max_lds;
+// LDS plan of one sweep launch: how many program steps of P-matrices (and
+// matching dL/dP accumulators) one LDS chunk holds.
+struct LdsPlan {
+  int cs;
+  size_t bytes;
+};
+
+LdsPlan plan_lds(const phy_ctx* c) {
+  const size_t cap = 160 * 1024;
+  const size_t budget = std::min<size_t>(cap, (size_t)c->lds_budget);
+  int cs = c->nsteps;
+  while (cs > 1 && lds_bytes(c->S, c->C, c->depth, cs) > budget) --cs;
+  LdsPlan p;
+  p.cs = cs;
+  p.bytes = lds_bytes(c->S, c->C, c->depth, cs);
+  return p;
 }
 
 int launch(phy_ctx* ctx, int n, const double* d_blens, const double* d_model, double* d_out,
            double* d_site, hipStream_t st) {
   const int C = ctx->C, B = ctx->B;
   {
-    PmatArgs pa{d_model, d_blens, ctx->d_pm, ctx->d_qp, C, B, ctx->kind};
+    PmatArgs pa{d_model, d_blens, ctx->d_gpos, ctx->d_pprog, ctx->d_qp, C, B, ctx->kind, ctx->nsteps,
+                ctx->merged_pos};
     hipLaunchKernelGGL(pmat_kernel, dim3(n), dim3(256), 0, st, pa);
     HIP_TRY(hipGetLastError());
   }
   const int gx = std::max(1, std::min(ctx->nblk, (ctx->wg_budget + n - 1) / n));
   if ((size_t)gx * n > (size_t)ctx->wg_cap) return fail(PHY_ERANGE, "workgroup cap exceeded");
-  const bool glds = use_glds(ctx);
-  const size_t lds = lds_bytes(ctx->S, C, B, ctx->depth, glds);
-  SweepArgs sa{ctx->d_tips, ctx->d_w,       ctx->d_prog, ctx->d_pm,     d_model,
-               ctx->d_scratch, ctx->d_gslot, ctx->d_sslot, d_site,       ctx->S,
-               ctx->P,       ctx->Ppad,    C,           B,             ctx->nsteps,
-               ctx->nslots,  ctx->nblk,    ctx->depth};
+  const LdsPlan plan = plan_lds(ctx);
+  const size_t lds = plan.bytes;
+  SweepArgs sa{ctx->d_tips,  ctx->d_w,      ctx->d_pprog, d_model,     ctx->d_scratch,
+               ctx->d_gslot, ctx->d_sslot,  d_site,       ctx->d_stamps, ctx->S,      ctx->P,
+               ctx->Ppad,    C,             ctx->nsteps,  ctx->nslots, ctx->nblk,
+               ctx->depth,   plan.cs};
   hipEvent_t e0 = nullptr, e1 = nullptr;
   if (ctx->timing) {
     if (ctx->ev_used + 2 > (int)ctx->ev.size()) {
@@ -801,22 +1116,20 @@ int launch(phy_ctx* ctx, int n, const double* d_blens, const double* d_model, do
     HIP_TRY(hipEventRecord(e0, st));
   }
   const int threads = C * WAVE;
-  if (threads <= 256) {
-    if (glds)
-      hipLaunchKernelGGL((sweep_kernel<true, 256>), dim3(gx, n), dim3(threads), lds, st, sa);
-    else
-      hipLaunchKernelGGL((sweep_kernel<false, 256>), dim3(gx, n), dim3(threads), lds, st, sa);
-  } else {
-    if (glds)
-      hipLaunchKernelGGL((sweep_kernel<true, 1024>), dim3(gx, n), dim3(threads), lds, st, sa);
-    else
-      hipLaunchKernelGGL((sweep_kernel<false, 1024>), dim3(gx, n), dim3(threads), lds, st, sa);
-  }
+  if (threads <= 256)
+    hipLaunchKernelGGL((sweep_kernel<256>), dim3(gx, n), dim3(threads), lds, st, sa, ctx->d_prog);
+  else if (threads <= 512)
+    hipLaunchKernelGGL((sweep_kernel<512>), dim3(gx, n), dim3(threads), lds, st, sa, ctx->d_prog);
+  else
+    hipLaunchKernelGGL((sweep_kernel<1024>), dim3(gx, n), dim3(threads), lds, st, sa, ctx->d_prog);
   HIP_TRY(hipGetLastError());
   if (ctx->timing) HIP_TRY(hipEventRecord(e1, st));
-  FinArgs fa{ctx->d_gslot, ctx->d_sslot, ctx->d_qp, d_blens, d_model, d_out, C, B, gx,
-             phy_output_len(ctx)};
-  hipLaunchKernelGGL(finalize_kernel, dim3(n), dim3(256), (size_t)C * B * sizeof(double), st, fa);
+  FinArgs fa{ctx->d_gslot, ctx->d_sslot, ctx->d_qp, d_blens, d_model, ctx->d_gpos, d_out,
+             C,            B,            ctx->nsteps, gx, phy_output_len(ctx)};
+  hipLaunchKernelGGL(finalize_g_kernel, dim3((C * B * 16 + 63) / 64, n), dim3(256), 0, st, fa);
+  HIP_TRY(hipGetLastError());
+  hipLaunchKernelGGL(finalize_s_kernel, dim3(n), dim3(256), ((size_t)C * B + B + 256) * sizeof(double), st,
+                     fa);
   HIP_TRY(hipGetLastError());
   return PHY_OK;
 }
@@ -866,6 +1179,8 @@ int phy_create(int S, int P, int C, int rooted, int model, const uint8_t* tipcod
   c->nsteps = S - 1;
   c->g_mode = 0;
   {
+    const char* lb = getenv("PHY_LDS_BUDGET");
+    c->lds_budget = lb ? std::max(16384, atoi(lb)) : 160 * 1024;
     const char* env = getenv("PHY_WG_BUDGET");
     c->wg_budget = env ? std::max(1, atoi(env)) : 512;
     const char* gm = getenv("PHY_G_MODE");
@@ -879,8 +1194,17 @@ int phy_create(int S, int P, int C, int rooted, int model, const uint8_t* tipcod
   }
   int lds_max = 0;
   (void)hipDeviceGetAttribute(&lds_max, hipDeviceAttributeMaxSharedMemoryPerBlock, device);
+  // gfx950: one workgroup may use the whole 160 KiB LDS; dynamic LDS above
+  // 64 KiB has to be opted into per kernel.
   c->max_lds = 65536;
-  if (lds_bytes(S, C, c->B, c->depth, false) > (size_t)std::max(lds_max, 65536)) {
+  {
+    const int cap = 160 * 1024;
+    const void* ks[] = {(const void*)sweep_kernel<256>, (const void*)sweep_kernel<512>,
+                        (const void*)sweep_kernel<1024>};
+    for (const void* k : ks) (void)hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, cap);
+    lds_max = std::max(lds_max, cap);
+  }
+  if (lds_bytes(S, C, c->depth, 1) > (size_t)lds_max) {
     delete c;
     return fail(PHY_EINVAL, "tree too deep for the LDS stack");
   }
@@ -907,15 +1231,17 @@ int phy_create(int S, int P, int C, int rooted, int model, const uint8_t* tipcod
   TRY_C(dalloc(&c->d_tips, (size_t)S * c->Ppad));
   TRY_C(dalloc(&c->d_w, (size_t)c->Ppad));
   TRY_C(dalloc(&c->d_prog, prog.size()));
-  TRY_C(dalloc(&c->d_pm, (size_t)max_draws * C * c->B * 16));
+  TRY_C(dalloc(&c->d_pprog, (size_t)max_draws * C * c->nsteps * 32));
   TRY_C(dalloc(&c->d_qp, (size_t)max_draws * C * c->B * 16));
   TRY_C(dalloc(&c->d_model, (size_t)max_draws * (10 + 2 * C)));
   TRY_C(dalloc(&c->d_blens, (size_t)max_draws * c->B));
   TRY_C(dalloc(&c->d_out, (size_t)max_draws * phy_output_len(c)));
   TRY_C(dalloc(&c->d_site, (size_t)max_draws * P));
   TRY_C(dalloc(&c->d_scratch, (size_t)c->wg_cap * std::max(c->nslots, 1) * 2 * ncolwg));
-  TRY_C(dalloc(&c->d_gslot, (size_t)c->wg_cap * C * c->B * 16));
+  TRY_C(dalloc(&c->d_gslot, (size_t)c->wg_cap * C * c->nsteps * 32));
+  TRY_C(dalloc(&c->d_gpos, (size_t)c->B));
   TRY_C(dalloc(&c->d_sslot, (size_t)c->wg_cap * C * 8));
+  if (PHY_STAMP) TRY_C(dalloc(&c->d_stamps, (size_t)c->wg_cap * C * 8));
   {
     std::vector<uint8_t> tips((size_t)S * c->Ppad, 15);
     for (int t = 0; t < S; ++t)
@@ -925,6 +1251,23 @@ int phy_create(int S, int P, int C, int rooted, int model, const uint8_t* tipcod
     HIP_C(hipMemcpy(c->d_tips, tips.data(), tips.size(), hipMemcpyHostToDevice));
     HIP_C(hipMemcpy(c->d_w, w.data(), w.size() * sizeof(double), hipMemcpyHostToDevice));
     HIP_C(hipMemcpy(c->d_prog, prog.data(), prog.size() * sizeof(int), hipMemcpyHostToDevice));
+    std::vector<int> gpos(c->B, -1);
+    for (int st = 0; st < c->nsteps; ++st)
+      for (int w = 0; w < 2; ++w) {
+        const int b = prog[(size_t)st * STEP_INTS + 2 + w];
+        if (b >= 0) gpos[b] = st * 2 + w;
+      }
+    c->merged_pos = -1;
+    for (int st = 0; st < c->nsteps; ++st)
+      for (int w = 0; w < 2; ++w)
+        if (prog[(size_t)st * STEP_INTS + 2 + w] < 0) c->merged_pos = st * 2 + w;
+    for (int b = 0; b < c->B; ++b)
+      if (gpos[b] < 0) {
+        std::string m_ = "internal: branch " + std::to_string(b) + " not in the program";
+        free_ctx(c);
+        return fail(PHY_EINVAL, m_);
+      }
+    HIP_C(hipMemcpy(c->d_gpos, gpos.data(), gpos.size() * sizeof(int), hipMemcpyHostToDevice));
   }
   *out = c;
   return PHY_OK;
@@ -1033,7 +1376,7 @@ int phy_timing_read(phy_ctx* ctx, double* total_ms, int* launches) {
   return PHY_OK;
 }
 
-int phy_set_tuning(phy_ctx* ctx, int wg_budget, int g_mode) {
+int phy_set_tuning(phy_ctx* ctx, int wg_budget, int g_mode, int lds_budget) {
   if (!ctx) return fail(PHY_EINVAL, "NULL ctx");
   if (wg_budget > 0) {
     const long need = std::min<long>((long)ctx->nblk * ctx->max_draws, (long)wg_budget + ctx->max_draws);
@@ -1042,6 +1385,27 @@ int phy_set_tuning(phy_ctx* ctx, int wg_budget, int g_mode) {
   }
   if (g_mode < 0 || g_mode > 2) return fail(PHY_EINVAL, "g_mode must be 0, 1 or 2");
   ctx->g_mode = g_mode;
+  if (lds_budget > 0) ctx->lds_budget = std::max(16384, std::min(lds_budget, 160 * 1024));
+  return PHY_OK;
+}
+
+// Diagnostic builds (-DPHY_STAMP=1): copy the per-wave s_memtime stamps of
+// the last launch ([wg][C][8]: start, fwd, root, rev, end-of-block, end,
+// realtime start, realtime end).  Returns the number of values copied.
+int phy_debug_stamps(phy_ctx* ctx, unsigned long long* out, int n) {
+  if (!ctx || !ctx->d_stamps) return 0;
+  const int m = std::min(n, ctx->wg_cap * ctx->C * 8);
+  if (hipMemcpy(out, ctx->d_stamps, sizeof(unsigned long long) * m, hipMemcpyDeviceToHost) != hipSuccess)
+    return 0;
+  return m;
+}
+
+int phy_lds_plan(const phy_ctx* ctx, int* g_in_lds, int* chunk_steps, int* lds_bytes_out) {
+  if (!ctx) return fail(PHY_EINVAL, "NULL ctx");
+  const LdsPlan p = plan_lds(ctx);
+  if (g_in_lds) *g_in_lds = 1;
+  if (chunk_steps) *chunk_steps = p.cs;
+  if (lds_bytes_out) *lds_bytes_out = (int)p.bytes;
   return PHY_OK;
 }
 

@@ -155,8 +155,14 @@ class TreeLikelihood:
     def sync(self):
         _lib.check(self.lib.phy_sync(self.ctx), "phy_sync")
 
-    def set_tuning(self, wg_budget=0, g_mode=0):
-        _lib.check(self.lib.phy_set_tuning(self.ctx, int(wg_budget), int(g_mode)), "phy_set_tuning")
+    def set_tuning(self, wg_budget=0, g_mode=0, lds_budget=0):
+        _lib.check(self.lib.phy_set_tuning(self.ctx, int(wg_budget), int(g_mode), int(lds_budget)),
+                   "phy_set_tuning")
+
+    def lds_plan(self):
+        vals = [ctypes.c_int() for _ in range(3)]
+        _lib.check(self.lib.phy_lds_plan(self.ctx, *[ctypes.byref(v) for v in vals]), "phy_lds_plan")
+        return dict(zip(("g_in_lds", "chunk_steps", "lds_bytes"), [v.value for v in vals]))
 
     def timing_start(self):
         _lib.check(self.lib.phy_timing_start(self.ctx), "phy_timing_start")

@@ -82,11 +82,15 @@ def test_all_ambiguous_and_padding():
     check_case(case)
 
 
-@pytest.mark.parametrize("g_mode", [1, 2])
-def test_g_modes(g_mode):
+@pytest.mark.parametrize("g_mode,lds_budget", [(1, 0), (2, 0), (2, 40000), (0, 24000), (1, 24000)])
+def test_lds_plans(g_mode, lds_budget):
+    """dL/dP in LDS / global, whole-program and chunked P-matrix staging."""
     case = cases.fluA_case()
     eng = _engine(case)
-    eng.set_tuning(0, g_mode)
+    eng.set_tuning(0, g_mode, lds_budget)
+    plan = eng.lds_plan()
+    if lds_budget:
+        assert plan["chunk_steps"] < case.S - 1
     check_case(case, eng)
 
 
