@@ -136,6 +136,12 @@ int phy_set_tuning(phy_ctx* ctx, int wg_budget, int g_mode, int lds_budget);
  * P-matrices per LDS chunk, LDS bytes per workgroup. */
 int phy_lds_plan(const phy_ctx* ctx, int* g_in_lds, int* chunk_steps, int* lds_bytes);
 
+/* Diagnostic builds only (-DPHY_STAMP=1): per-wave s_memtime stamps of the
+ * last launch, [wg][C][8] = start, forward, root, reverse, end of first
+ * block, end, realtime start, realtime end.  Returns values copied (0 in
+ * normal builds). */
+int phy_debug_stamps(phy_ctx* ctx, unsigned long long* out, int n);
+
 #ifdef __cplusplus
 }
 #endif
