@@ -126,15 +126,15 @@ int phy_sync(phy_ctx* ctx);
 int phy_timing_start(phy_ctx* ctx);
 int phy_timing_read(phy_ctx* ctx, double* total_ms, int* launches);
 
-/* Tuning: persistent workgroup budget per launch (0 = keep), where the dL/dP
- * partial sums live (0 auto, 1 LDS, 2 global) and the LDS bytes one
- * workgroup may use (0 = keep; default 160 KiB; smaller budgets stage the
- * P-matrices in more chunks and admit more workgroups per CU). */
+/* Tuning: persistent workgroup budget per launch (0 = keep), g_mode
+ * (reserved, must be 0..2) and the LDS bytes one workgroup may use (0 =
+ * keep; default 80 KiB = two workgroups per CU; smaller budgets stage the
+ * P-matrices and dL/dP accumulators in more chunks). */
 int phy_set_tuning(phy_ctx* ctx, int wg_budget, int g_mode, int lds_budget);
 
-/* The LDS plan the next launch will use: dL/dP in LDS?, program steps of
- * P-matrices per LDS chunk, LDS bytes per workgroup. */
-int phy_lds_plan(const phy_ctx* ctx, int* g_in_lds, int* chunk_steps, int* lds_bytes);
+/* The LDS plan the next launch will use: chunks per pass, matrices per
+ * chunk, LDS bytes per workgroup. */
+int phy_lds_plan(const phy_ctx* ctx, int* n_chunks, int* matrices_per_chunk, int* lds_bytes);
 
 /* Diagnostic builds only (-DPHY_STAMP=1): per-wave s_memtime stamps of the
  * last launch, [wg][C][8] = start, forward, root, reverse, end of first

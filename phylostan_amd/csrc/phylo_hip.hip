@@ -11,25 +11,28 @@
 //
 // Design (DESIGN.md has the long form):
 //   One lane = one (pattern, category) column, one wave = 64 patterns of ONE
-//   category (so every P-matrix a wave touches is wave-uniform and is read
-//   with scalar loads), one workgroup = the C category-waves of a 64-pattern
-//   block (so the per-site mixture sum sum_c ps_c pi.p_root,c is an LDS
-//   exchange, not a global one).  Workgroups are persistent over pattern
-//   blocks.  Per block:
+//   category (every P-matrix a wave touches is wave-uniform: LDS broadcast
+//   reads), one workgroup = the C category-waves of a 64-pattern block (the
+//   per-site mixture sum sum_c ps_c pi.p_root,c is an LDS exchange).
+//   Workgroups are persistent over pattern blocks.  Per block:
 //     forward  -- walks a host-built post-order program whose child order
-//                 minimises the stack (Strahler order); pending partials live
-//                 on a per-lane LDS stack; every non-root internal partial is
-//                 also written once to a per-workgroup scratch region
-//                 (fp64, 16 B per lane per store, coalesced);
+//                 minimises the stack (Strahler order).  Step v turns its
+//                 children's "moved" partials a = P p into p_v = a_x * a_y
+//                 and its own a_v = P_v p_v; a_v goes on a per-lane LDS stack
+//                 and, once, to a per-workgroup HBM scratch region (fp64,
+//                 16 B per lane per store, coalesced);
 //     root     -- mixture sum through LDS, site log-likelihood, w/L scale;
-//     reverse  -- walks the program backwards carrying the pre-order upper
-//                 partial q on the LDS stack; reads each stored partial
-//                 exactly once; accumulates dlogL/dP per (branch, category)
-//                 by a 64-lane transpose-reduce into LDS or a workgroup-
-//                 private global slot.
-//   A finalize kernel sums the per-workgroup slots in a fixed order
-//   (bitwise deterministic) and applies dP/dt = Q P for the branch-length
-//   and rate gradients.
+//     reverse  -- walks the program backwards carrying the upper partial r
+//                 of each branch on the stack: q_v = P_v^T r_v,
+//                 r_x = q_v * a_y, and dL/dP_v += r_v (x) (a_x * a_y).  Each
+//                 stored a is read exactly once (buffer-descriptor prefetch,
+//                 one step ahead); dL/dP is reduced over the wave with
+//                 permlane/DPP ops into an LDS accumulator.
+//   P-matrices and their dL/dP accumulators are staged in LDS in chunks of
+//   the program ("matrices in order of use"), sized to the LDS budget.
+//   Finalize kernels sum the per-workgroup slots in a fixed order (bitwise
+//   deterministic) and apply dP/dt = Q P for the branch-length and rate
+//   gradients.
 //
 // fp64 throughout, no rescaling -- exactly as the reference
 // (generate_script.py:995, :1010); parity target 1e-6 relative per site.
@@ -52,7 +55,12 @@ constexpr int WAVE = 64;
 #ifndef PHY_ABLATE
 #define PHY_ABLATE 0  // diagnostic builds only: 1 no dL/dP accumulation, 2 no reverse pass, 4 no scratch stores
 #endif
-constexpr int STEP_INTS = 8;  // x, y, bx, by, vslot, pad...
+// Program step (8 ints): x, y (child codes: tip index >= 0, or -(slot+1) of
+// an internal child's stored moved partial), mx, my (matrix of a tip child,
+// -1 if internal), mv (matrix of the step's own branch, -1 at the root),
+// vslot (scratch slot of a_v, -1 at the root), flags (bit 0: mv is a real
+// branch, not the merged identity), node id.
+constexpr int STEP_INTS = 8;
 
 thread_local std::string g_err;
 
@@ -229,14 +237,14 @@ __device__ __forceinline__ int reduce16_entry(int lane) {
 struct SweepArgs {
   const uint8_t* tips;    // [S][Ppad] state masks
   const double* weights;  // [Ppad]   (0 on padding)
-  const double* pprog;    // [draw][C][nsteps][2][16]  P of both children, program order
+  const double* pmat;     // [draw][C][nmat][16]  P of every branch, in program-use order
   const double* model;    // [draw][10+2C]
-  double2* scratch;       // [wg][nslots][2][C*64]
-  double* gslot;          // [wg][C][nsteps][2][16]  dL/dP partial sums, program order
+  double2* scratch;       // [wg][nslots][2][C*64]   stored moved partials
+  double* gslot;          // [wg][C][nmat][16]       dL/dP partial sums, program-use order
   double* sslot;          // [wg][C][8]
   double* site_ll;        // [draw][P] or null
   unsigned long long* stamps;  // diagnostic builds (PHY_STAMP): [wg][C][8] s_memtime
-  int S, P, Ppad, C, nsteps, nslots, nblk, depth, cs;
+  int S, P, Ppad, C, nsteps, nslots, nblk, depth, nmat, cap_m;
 };
 
 #ifndef PHY_STAMP
@@ -249,13 +257,13 @@ struct SweepArgs {
   } while (0)
 
 // LDS carve (all offsets multiples of 16 B):
-//   P chunk  C * cs * 32 double   (both children's matrices of steps [s0, s0+cs))
-//   G chunk  C * cs * 32 double   (dL/dP of the same branches)
+//   P chunk  C * cap_m * 16 double   (matrices [mstart, mstart+cap_m) of the chunk)
+//   G chunk  C * cap_m * 16 double   (their dL/dP accumulators)
 //   stacks   C * depth * 2 * 64 double2
 //   tips     S * 64 bytes (rounded to 16)
 //   rootL    C * 64 double
-__host__ __device__ inline size_t lds_bytes(int S, int C, int depth, int cs) {
-  size_t b = 2 * (size_t)C * cs * 32 * 8;
+__host__ __device__ inline size_t lds_bytes(int S, int C, int depth, int cap_m) {
+  size_t b = 2 * (size_t)C * cap_m * 16 * 8;
   b += (size_t)C * depth * 2 * WAVE * 16;
   b += ((size_t)S * WAVE + 15) / 16 * 16;
   b += (size_t)C * WAVE * 8;
@@ -276,66 +284,70 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* base, ui
   return __builtin_amdgcn_make_buffer_rsrc(p, (short)0, (int)n, 0x00020000);
 }
 
-// `prog` is a separate __restrict__ const argument so the backend can prove
-// it is never written and read it with scalar (s_load) instructions; inside
-// the struct it would be read with vector loads + a full vmcnt(0) per step.
+// s_waitcnt vmcnt(0) that the compiler's waitcnt pass sees (an inline-asm
+// wait would be invisible to it): clears the loads the previous block's
+// reverse pass left pending, so the forward loop body is not charged a
+// loop-carried vmcnt(0) on every step.
+#define WAIT_VMCNT0() __builtin_amdgcn_s_waitcnt(0x0F70)
+
+// `prog`, `chunk_of` and `chunk_m0` are separate __restrict__ const
+// arguments so the backend proves them read-only and uses scalar loads.
 template <int MAXT>
-__global__ void __launch_bounds__(MAXT) sweep_kernel(SweepArgs a, const int* __restrict__ prog) {
+__global__ void __launch_bounds__(MAXT)
+    sweep_kernel(SweepArgs a, const int* __restrict__ prog, const int* __restrict__ chunk_of,
+                 const int* __restrict__ chunk_m0) {
   extern __shared__ __attribute__((aligned(16))) unsigned char lds_raw[];
   const int lane = threadIdx.x & (WAVE - 1);
   const int c = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int nthreads = blockDim.x;
   const int draw = blockIdx.y;
   const int wg = blockIdx.y * gridDim.x + blockIdx.x;
-  const int C = a.C, cs = a.cs, nsteps = a.nsteps;
+  const int C = a.C, nsteps = a.nsteps, nmat = a.nmat, cap_m = a.cap_m;
   const int ncolwg = C * WAVE;
-  const bool one_chunk = cs >= nsteps;
+  const bool one_chunk = chunk_of[0] == chunk_of[nsteps - 1];
   bool blk0 = true;  // first pattern block of this workgroup (diagnostic stamps)
   if (PHY_STAMP && a.stamps && lane == 0) {
     a.stamps[((size_t)wg * C + c) * 8 + 6] = __builtin_amdgcn_s_memrealtime();
     a.stamps[((size_t)wg * C + c) * 8 + 0] = __builtin_amdgcn_s_memtime();
   }
 
-  double* pl = reinterpret_cast<double*>(lds_raw);  // [C][cs][2][16]
-  double* gl = pl + (size_t)C * cs * 32;             // [C][cs][2][16]
-  double2* stk = reinterpret_cast<double2*>(gl + (size_t)C * cs * 32) + (size_t)c * a.depth * 2 * WAVE;
-  unsigned char* tipl = reinterpret_cast<unsigned char*>(gl + (size_t)C * cs * 32) +
+  double* pl = reinterpret_cast<double*>(lds_raw);  // [C][cap_m][16]
+  double* gl = pl + (size_t)C * cap_m * 16;          // [C][cap_m][16]
+  double2* stk = reinterpret_cast<double2*>(gl + (size_t)C * cap_m * 16) + (size_t)c * a.depth * 2 * WAVE;
+  unsigned char* tipl = reinterpret_cast<unsigned char*>(gl + (size_t)C * cap_m * 16) +
                         (size_t)C * a.depth * 2 * WAVE * 16;
   double* rootL = reinterpret_cast<double*>(tipl + ((size_t)a.S * WAVE + 15) / 16 * 16);
 
   const double* mdl = a.model + (size_t)draw * (10 + 2 * C);
   const V4 pi = {mdl[0], mdl[1], mdl[2], mdl[3]};
   const double ps_c = mdl[10 + C + c];
-  const double* pprog_d = a.pprog + (size_t)draw * C * nsteps * 32;
+  const double* pmat_d = a.pmat + (size_t)draw * C * nmat * 16;
   double2* scr = a.scratch + (size_t)wg * a.nslots * 2 * ncolwg;
-  double* gslot_wg = a.gslot + (size_t)wg * C * nsteps * 32;
+  double* gslot_wg = a.gslot + (size_t)wg * C * nmat * 16;
   const uint32_t scr_bytes = (uint32_t)((size_t)a.nslots * 2 * ncolwg * 16);
   const __amdgpu_buffer_rsrc_t srd = make_rsrc(scr, scr_bytes);
 
   const int e = reduce16_entry(lane);
   const bool gowner = (lane & 3) == 0;
 
-  for (int k = threadIdx.x; k < C * cs * 32; k += nthreads) gl[k] = 0.0;
+  for (int k = threadIdx.x; k < C * cap_m * 16; k += nthreads) gl[k] = 0.0;
 
   double acc_ll = 0.0, acc_dps = 0.0;
   V4 acc_f = {0.0, 0.0, 0.0, 0.0};
 
-  // P-matrices (and the matching dL/dP accumulators) live in LDS, in chunks
-  // of cs program steps; one chunk = the whole program when it fits, staged
-  // once per workgroup.  Reads use wave-uniform LDS addresses (broadcast).
-  int chunk_lo = -1;
+  // ---- P-matrix / dL/dP chunks in LDS ----
+  int cur = -1, m0 = 0, mcount = 0;
   // Hand the LDS G chunk to this workgroup's global slot and zero it: a
   // plain store the first time the slot region is written (the workgroup's
-  // first pattern block), otherwise load-add-store with 8 loads in flight
-  // per thread.
+  // first pattern block), otherwise load-add-store, 8 loads in flight per
+  // thread.
   bool g_first = true;
   auto flush_g = [&]() {
-    if (chunk_lo < 0) return;
-    const int n = min(cs, nsteps - chunk_lo);
-    const int q = n * 32;  // doubles per category
+    if (cur < 0) return;
+    const int q = mcount * 16;  // doubles per category
     for (int cc = 0; cc < C; ++cc) {
-      double* gp = gslot_wg + ((size_t)cc * nsteps + chunk_lo) * 32;
-      double* lp = gl + (size_t)cc * cs * 32;
+      double* gp = gslot_wg + ((size_t)cc * nmat + m0) * 16;
+      double* lp = gl + (size_t)cc * cap_m * 16;
       for (int k0 = threadIdx.x; k0 < q; k0 += nthreads * 8) {
         double old[8];
 #pragma unroll
@@ -353,20 +365,20 @@ __global__ void __launch_bounds__(MAXT) sweep_kernel(SweepArgs a, const int* __r
         }
       }
     }
+    WAIT_VMCNT0();
   };
   auto ensure_chunk = [&](int s, bool reverse) {
-    const int lo = (s / cs) * cs;
-    if (lo == chunk_lo) return;  // workgroup-uniform
+    const int ch = chunk_of[s];
+    if (ch == cur) return;  // workgroup-uniform
     __syncthreads();
     if (reverse) flush_g();
-    // per category the chunk is one contiguous run of n*32 doubles; 8 loads
-    // in flight per thread before the LDS writes (a load->write loop would
-    // serialise one memory round trip per element)
-    const int n = min(cs, nsteps - lo);
-    const int q2 = n * 16;  // double2 per category
+    const int lo = chunk_m0[ch], n = chunk_m0[ch + 1] - lo;
+    // per category one contiguous run of n*16 doubles; 8 loads in flight
+    // per thread before the LDS writes
+    const int q2 = n * 8;  // double2 per category
     for (int cc = 0; cc < C; ++cc) {
-      const double2* src = reinterpret_cast<const double2*>(pprog_d + ((size_t)cc * nsteps + lo) * 32);
-      double2* dst = reinterpret_cast<double2*>(pl + (size_t)cc * cs * 32);
+      const double2* src = reinterpret_cast<const double2*>(pmat_d + ((size_t)cc * nmat + lo) * 16);
+      double2* dst = reinterpret_cast<double2*>(pl + (size_t)cc * cap_m * 16);
       for (int k0 = threadIdx.x; k0 < q2; k0 += nthreads * 8) {
         double2 buf[8];
 #pragma unroll
@@ -381,12 +393,13 @@ __global__ void __launch_bounds__(MAXT) sweep_kernel(SweepArgs a, const int* __r
         }
       }
     }
+    WAIT_VMCNT0();  // no staging load may look pending inside the step loops
     __syncthreads();
-    chunk_lo = lo;
+    cur = ch;
+    m0 = lo;
+    mcount = n;
   };
-  auto pmat = [&](int s, int which) -> const double* {
-    return pl + ((size_t)c * cs + (s - chunk_lo)) * 32 + which * 16;
-  };
+  auto pm = [&](int m) -> const double* { return pl + ((size_t)c * cap_m + (m - m0)) * 16; };
 
   // Pending-vector stack: the most recent entry stays in registers (most
   // pushes are popped by the very next step), older ones live in LDS.
@@ -415,9 +428,9 @@ __global__ void __launch_bounds__(MAXT) sweep_kernel(SweepArgs a, const int* __r
     const double2 hi = stk[(sp * 2 + 1) * WAVE + lane];
     return {lo.x, lo.y, hi.x, hi.y};
   };
-  // dL/dP_{branch of (s, which)} += r (x) p, reduced over the wave; the lane
-  // owning entry e adds it to the LDS G chunk (one lane per address)
-  auto gacc = [&](int s, int which, const V4& r, const V4& p) {
+  // dL/dP_m += r (x) p, reduced over the wave; the lane owning entry e adds
+  // it to the LDS G chunk (one lane per address: plain read-add-write)
+  auto gacc = [&](int m, const V4& r, const V4& p) {
     double v[16] = {r.x * p.x, r.x * p.y, r.x * p.z, r.x * p.w, r.y * p.x, r.y * p.y,
                     r.y * p.z, r.y * p.w, r.z * p.x, r.z * p.y, r.z * p.z, r.z * p.w,
                     r.w * p.x, r.w * p.y, r.w * p.z, r.w * p.w};
@@ -426,13 +439,13 @@ __global__ void __launch_bounds__(MAXT) sweep_kernel(SweepArgs a, const int* __r
       return;
     }
     const double sum = reduce16(v, lane);
-    if (gowner) gl[((size_t)c * cs + (s - chunk_lo)) * 32 + which * 16 + e] += sum;
+    if (gowner) gl[((size_t)c * cap_m + (m - m0)) * 16 + e] += sum;
   };
 
   for (int blk = blockIdx.x; blk < a.nblk; blk += gridDim.x) {
     const int i = blk * WAVE + lane;  // pattern of this lane
     // stage this block's tip codes in LDS: S rows x 64 bytes, shared by the
-    // C category-waves and by both passes
+    // C category-waves and by both passes (8 loads in flight per thread)
     {
       const uint32_t* src = reinterpret_cast<const uint32_t*>(a.tips);
       uint32_t* dst = reinterpret_cast<uint32_t*>(tipl);
@@ -453,6 +466,7 @@ __global__ void __launch_bounds__(MAXT) sweep_kernel(SweepArgs a, const int* __r
       }
     }
     __syncthreads();
+    WAIT_VMCNT0();
 
     STAMP(1);
     // ------------------------------ forward ------------------------------
@@ -462,19 +476,18 @@ __global__ void __launch_bounds__(MAXT) sweep_kernel(SweepArgs a, const int* __r
     for (int s = 0; s < nsteps; ++s) {
       ensure_chunk(s, false);
       const int* st = prog + s * STEP_INTS;
-      const int x = st[0], y = st[1], vs = st[4];
-      const V4 cy = (y >= 0) ? tipvec(tipl[y * WAVE + lane]) : pop();
-      const V4 ay = matvec_p(pmat(s, 1), cy);  // identity for a merged branch
-      const V4 cx = (x >= 0) ? tipvec(tipl[x * WAVE + lane]) : pop();
-      const V4 ax = matvec_p(pmat(s, 0), cx);
+      const int x = st[0], y = st[1], mx = st[2], my = st[3], mv = st[4], vs = st[5], fl = st[6];
+      const V4 ay = (y >= 0) ? matvec_p(pm(my), tipvec(tipl[y * WAVE + lane])) : pop();
+      const V4 ax = (x >= 0) ? matvec_p(pm(mx), tipvec(tipl[x * WAVE + lane])) : pop();
       const V4 pv = vmul(ax, ay);
       if (vs >= 0) {
+        const V4 av = (fl & 1) ? matvec_p(pm(mv), pv) : pv;  // merged root branch: identity
         if (!(PHY_ABLATE & 4)) {
           double2* dst = scr + (size_t)vs * 2 * ncolwg + c * WAVE + lane;
-          dst[0] = make_double2(pv.x, pv.y);
-          dst[ncolwg] = make_double2(pv.z, pv.w);
+          dst[0] = make_double2(av.x, av.y);
+          dst[ncolwg] = make_double2(av.z, av.w);
         }
-        push(pv);
+        push(av);
       } else {
         proot = pv;
       }
@@ -504,10 +517,10 @@ __global__ void __launch_bounds__(MAXT) sweep_kernel(SweepArgs a, const int* __r
 
     STAMP(3);
     // ------------------------------ reverse ------------------------------
-    // Software-pipelined one step deep: the children of step s-1 are
-    // requested before step s is computed.  Scratch partials come through
-    // the buffer descriptor; a tip child gets an out-of-range offset (the
-    // load returns 0 and moves no data) and its code is read from LDS.
+    // Upper partials r travel down the stack.  Software-pipelined one step
+    // deep: the stored moved partials of step s-1's children are requested
+    // before step s is computed (buffer loads; a tip child gets an
+    // out-of-range offset: zeros, no memory traffic).
     sp = 0;
     has_top = false;
     const uint32_t col_off = (uint32_t)((c * WAVE + lane) * 16);
@@ -525,28 +538,38 @@ __global__ void __launch_bounds__(MAXT) sweep_kernel(SweepArgs a, const int* __r
       return r;
     };
     if (!(PHY_ABLATE & 2)) {
-      const int* st = prog + (nsteps - 1) * STEP_INTS;
-      int x = st[0], y = st[1];
+      const int* st0 = prog + (nsteps - 1) * STEP_INTS;
+      int x = st0[0], y = st0[1];
       V4 lx = ld_partial(ld_off(x)), ly = ld_partial(ld_off(y));
       unsigned tx = tipl[max(x, 0) * WAVE + lane], ty = tipl[max(y, 0) * WAVE + lane];
       for (int s = nsteps - 1; s >= 0; --s) {
         ensure_chunk(s, true);
         const int* sn = prog + max(s - 1, 0) * STEP_INTS;
-        const int nx = sn[0], ny = sn[1];
-        const V4 nlx = ld_partial(ld_off(nx)), nly = ld_partial(ld_off(ny));
+        const int nx = (s > 0) ? sn[0] : 0, ny = (s > 0) ? sn[1] : 0;
+        const V4 nlx = ld_partial(s > 0 ? ld_off(nx) : scr_bytes);
+        const V4 nly = ld_partial(s > 0 ? ld_off(ny) : scr_bytes);
         const unsigned ntx = tipl[max(nx, 0) * WAVE + lane], nty = tipl[max(ny, 0) * WAVE + lane];
-        const int* sc_ = prog + s * STEP_INTS;
-        const int bx = sc_[2], by = sc_[3];
-        const V4 px = (x >= 0) ? tipvec(tx) : lx;
-        const V4 py = (y >= 0) ? tipvec(ty) : ly;
-        const V4 qv = (s == nsteps - 1) ? pi : pop();
-        const V4 ax = matvec_p(pmat(s, 0), px);
-        const V4 rx = vmul(qv, matvec_p(pmat(s, 1), py));
+        const int* st = prog + s * STEP_INTS;
+        const int mx = st[2], my = st[3], mv = st[4], fl = st[6];
+        const V4 tvx = tipvec(tx), tvy = tipvec(ty);
+        const V4 ax = (x >= 0) ? matvec_p(pm(mx), tvx) : lx;
+        const V4 ay = (y >= 0) ? matvec_p(pm(my), tvy) : ly;
+        V4 qv = pi;
+        if (s != nsteps - 1) {
+          const V4 rv = pop();
+          if (fl & 1) {
+            qv = matTvec_p(pm(mv), rv);
+            gacc(mv, vscale(rv, s_c), vmul(ax, ay));  // dL/dP_v += r_v (x) p_v
+          } else {
+            qv = rv;  // merged root branch: identity
+          }
+        }
+        const V4 rx = vmul(qv, ay);
         const V4 ry = vmul(qv, ax);
-        if (x < 0) push(matTvec_p(pmat(s, 0), rx));
-        if (y < 0) push(matTvec_p(pmat(s, 1), ry));
-        if (bx >= 0) gacc(s, 0, vscale(rx, s_c), px);
-        if (by >= 0) gacc(s, 1, vscale(ry, s_c), py);
+        if (x < 0) push(rx);
+        if (y < 0) push(ry);
+        if (x >= 0) gacc(mx, vscale(rx, s_c), tvx);
+        if (y >= 0) gacc(my, vscale(ry, s_c), tvy);
         x = nx;
         y = ny;
         lx = nlx;
@@ -561,6 +584,7 @@ __global__ void __launch_bounds__(MAXT) sweep_kernel(SweepArgs a, const int* __r
         g_first = false;  // every chunk of the slot has now been written once
       }
     }
+    WAIT_VMCNT0();
     STAMP(4);
     blk0 = false;
     __syncthreads();  // tips / rootL are rewritten by the next block
@@ -596,12 +620,12 @@ __global__ void __launch_bounds__(MAXT) sweep_kernel(SweepArgs a, const int* __r
 // P-matrices (generate_script.py:755-892), one workgroup per draw
 // ---------------------------------------------------------------------------
 struct PmatArgs {
-  const double* model;  // [draw][10+2C]
-  const double* blens;  // [draw][B]
-  const int* gpos;      // [B] program position (step*2 + which) of branch b
-  double* pprog;        // [draw][C][nsteps][2][16]  program order (identity if merged)
-  double* qp;           // [draw][C][B][16]  Q P  (= dP/dt), branch order
-  int C, B, kind, nsteps, merged_pos;
+  const double* model;    // [draw][10+2C]
+  const double* blens;    // [draw][B]
+  const int* mat_branch;  // [nmat] branch (node id) of matrix m, -1 = identity
+  double* pmat;           // [draw][C][nmat][16]  program-use order
+  double* qp;             // [draw][C][B][16]  Q P  (= dP/dt), branch order
+  int C, B, kind, nmat;
 };
 
 // Cyclic Jacobi eigendecomposition of a symmetric 4x4 (A overwritten).
@@ -645,27 +669,30 @@ __device__ void jacobi4(double A[4][4], double V[4][4], double lam[4]) {
   for (int i = 0; i < 4; ++i) lam[i] = A[i][i];
 }
 
-constexpr int PM_ITEMS = 4;  // (category, branch) items per thread per round
+constexpr int PM_ITEMS = 4;  // (category, matrix) items per thread per round
 
 __global__ void __launch_bounds__(256) pmat_kernel(PmatArgs a) {
   __shared__ double m1[16], m2[16], lam[4], Q[16];
   const int draw = blockIdx.x;
-  const int C = a.C, B = a.B, nsteps = a.nsteps;
+  const int C = a.C, B = a.B, nmat = a.nmat;
   const double* mdl = a.model + (size_t)draw * (10 + 2 * C);
   const double* rs = mdl + 10;
   const double* bl = a.blens + (size_t)draw * B;
-  const int nitem = C * B;
-  // this thread's first round of items: branch times and program positions
-  // are requested before the eigendecomposition so their latency overlaps it
+  const int nitem = C * nmat;
+  // this thread's first round of items: branch ids and times are requested
+  // before the eigendecomposition so their latency overlaps it
   double tv[PM_ITEMS];
-  int pos[PM_ITEMS];
+  int br[PM_ITEMS];
+  auto fetch = [&](int base) {
 #pragma unroll
-  for (int u = 0; u < PM_ITEMS; ++u) {
-    const int idx = threadIdx.x + u * blockDim.x;
-    const int c = idx / B, b = idx - c * B;
-    tv[u] = (idx < nitem) ? bl[b] * rs[c] : 0.0;
-    pos[u] = (idx < nitem) ? a.gpos[b] : 0;
-  }
+    for (int u = 0; u < PM_ITEMS; ++u) {
+      const int idx = base + threadIdx.x + u * blockDim.x;
+      const int c = idx / nmat, m = idx - c * nmat;
+      br[u] = (idx < nitem) ? a.mat_branch[m] : -1;
+      tv[u] = (idx < nitem && br[u] >= 0) ? bl[br[u]] * rs[c] : 0.0;
+    }
+  };
+  fetch(0);
   if (threadIdx.x == 0) {
     if (a.kind == PHY_JC69) {
       for (int j = 0; j < 4; ++j)
@@ -690,10 +717,9 @@ __global__ void __launch_bounds__(256) pmat_kernel(PmatArgs a) {
       }
       double A[4][4], V[4][4], l[4], sq[4];
       for (int j = 0; j < 4; ++j) sq[j] = sqrt(f[j]);
-      const double inv_s = 1.0 / s;
       for (int j = 0; j < 4; ++j)
         for (int k = 0; k < 4; ++k) {
-          q[j][k] *= inv_s;  // :868
+          q[j][k] /= s;  // :868
           Q[j * 4 + k] = q[j][k];
         }
       for (int j = 0; j < 4; ++j)  // A = Pi^1/2 Q Pi^-1/2, symmetrised (:870)
@@ -708,30 +734,22 @@ __global__ void __launch_bounds__(256) pmat_kernel(PmatArgs a) {
         }
       }
     }
-    if (a.merged_pos >= 0)  // unrooted: the merged root branch (generate_script.py:1019)
-      for (int c = 0; c < C; ++c) {
-        double* po = a.pprog + (((size_t)draw * C + c) * nsteps * 2 + a.merged_pos) * 16;
-        for (int k = 0; k < 16; ++k) po[k] = (k % 5 == 0) ? 1.0 : 0.0;
-      }
   }
   __syncthreads();
   for (int base = 0; base < nitem; base += PM_ITEMS * blockDim.x) {
-    if (base > 0) {
-#pragma unroll
-      for (int u = 0; u < PM_ITEMS; ++u) {
-        const int idx = base + threadIdx.x + u * blockDim.x;
-        const int c = idx / B, b = idx - c * B;
-        tv[u] = (idx < nitem) ? bl[b] * rs[c] : 0.0;
-        pos[u] = (idx < nitem) ? a.gpos[b] : 0;
-      }
-    }
+    if (base > 0) fetch(base);
 #pragma unroll
     for (int u = 0; u < PM_ITEMS; ++u) {
       const int idx = base + threadIdx.x + u * blockDim.x;
       if (idx >= nitem) break;
-      const int c = idx / B, b = idx - c * B;
-      const double t = tv[u];
+      const int c = idx / nmat, m = idx - c * nmat;
       double P[16];
+      double* po = a.pmat + (((size_t)draw * C + c) * nmat + m) * 16;
+      if (br[u] < 0) {  // the merged root branch of an unrooted tree (generate_script.py:1019)
+        for (int k = 0; k < 16; ++k) po[k] = (k % 5 == 0) ? 1.0 : 0.0;
+        continue;
+      }
+      const double t = tv[u];
       if (a.kind == PHY_JC69) {  // generate_script.py:765-769
         const double ex = exp(-t / 0.75);
         const double off = 0.25 - 0.25 * ex, d = 0.25 + 0.75 * ex;
@@ -746,8 +764,7 @@ __global__ void __launch_bounds__(256) pmat_kernel(PmatArgs a) {
             P[j * 4 + k] = acc;
           }
       }
-      double* po = a.pprog + (((size_t)draw * C + c) * nsteps * 2 + pos[u]) * 16;
-      double* qo = a.qp + (((size_t)draw * C + c) * B + b) * 16;
+      double* qo = a.qp + (((size_t)draw * C + c) * B + br[u]) * 16;
       for (int k = 0; k < 16; ++k) po[k] = P[k];
       for (int j = 0; j < 4; ++j)
         for (int k = 0; k < 4; ++k) {
@@ -763,14 +780,14 @@ __global__ void __launch_bounds__(256) pmat_kernel(PmatArgs a) {
 // finalize: fixed-order sums of the per-workgroup slots + chain rule dP/dt
 // ---------------------------------------------------------------------------
 struct FinArgs {
-  const double* gslot;  // [wg][C][nsteps][2][16]  program order
+  const double* gslot;  // [wg][C][nmat][16]  program-use order
   const double* sslot;  // [wg][C][8]
   const double* qp;     // [draw][C][B][16]
   const double* blens;  // [draw][B]
   const double* model;  // [draw][10+2C]
-  const int* gpos;      // [B] step*2 + which of branch b
+  const int* gpos;      // [B] matrix index of branch b
   double* out;          // [draw][outlen]
-  int C, B, nsteps, gx, outlen;
+  int C, B, nmat, gx, outlen;
 };
 
 // dL/dP: out[draw][og + (c*B + b)*16 + k] = sum over the draw's workgroup
@@ -783,13 +800,13 @@ __global__ void __launch_bounds__(256) finalize_g_kernel(FinArgs a) {
   const int ng = C * B * 16;
   const int idx = blockIdx.x * 64 + (threadIdx.x & 63);
   const int grp = threadIdx.x >> 6;
-  const size_t per_wg = (size_t)C * a.nsteps * 32;
+  const size_t per_wg = (size_t)C * a.nmat * 16;
   const size_t wg0 = (size_t)draw * a.gx;
   double acc = 0.0;
   if (idx < ng) {
     const int c = idx / (B * 16), rem = idx - c * B * 16;
     const int b = rem >> 4, k = rem & 15;
-    const double* src = a.gslot + wg0 * per_wg + ((size_t)c * a.nsteps * 2 + a.gpos[b]) * 16 + k;
+    const double* src = a.gslot + wg0 * per_wg + ((size_t)c * a.nmat + a.gpos[b]) * 16 + k;
     for (int w0 = grp; w0 < a.gx; w0 += 4 * 8) {
       double v[8];
 #pragma unroll
@@ -888,14 +905,19 @@ __global__ void __launch_bounds__(256) finalize_s_kernel(FinArgs a) {
 // ---------------------------------------------------------------------------
 struct phy_ctx {
   int S, P, Ppad, C, B, rooted, kind, max_draws, device;
-  int nsteps, nslots, depth, nblk;
-  int wg_budget, g_mode, wg_cap, lds_budget, merged_pos;
+  int nsteps, nslots, depth, nblk, nmat;
+  int wg_budget, g_mode, wg_cap, lds_budget;
+  int cap_m = 0, nchunks = 0;  // current LDS plan
   hipStream_t stream;
+  std::vector<int> prog;  // host copy of the program
   uint8_t* d_tips = nullptr;
   double* d_w = nullptr;
   int* d_prog = nullptr;
   int* d_gpos = nullptr;
-  double* d_pprog = nullptr;
+  int* d_mat_branch = nullptr;
+  int* d_chunk_of = nullptr;
+  int* d_chunk_m0 = nullptr;
+  double* d_pmat = nullptr;
   double* d_qp = nullptr;
   double* d_model = nullptr;
   double* d_blens = nullptr;
@@ -910,7 +932,6 @@ struct phy_ctx {
   int ev_used = 0;
   double timed_ms = 0.0;
   int timed_n = 0;
-  int max_lds = 65536;
 };
 
 namespace {
@@ -920,8 +941,9 @@ void free_ctx(phy_ctx* c) {
   int dev_old = 0;
   (void)hipGetDevice(&dev_old);
   (void)hipSetDevice(c->device);
-  void* ptrs[] = {c->d_stamps, c->d_tips, c->d_w, c->d_prog, c->d_gpos, c->d_pprog, c->d_qp, c->d_model, c->d_blens,
-                  c->d_out, c->d_site, c->d_scratch, c->d_gslot, c->d_sslot};
+  void* ptrs[] = {c->d_tips,  c->d_w,     c->d_prog,    c->d_gpos,    c->d_mat_branch, c->d_chunk_of,
+                  c->d_chunk_m0, c->d_pmat, c->d_qp,    c->d_model,   c->d_blens,      c->d_out,
+                  c->d_site,  c->d_scratch, c->d_gslot, c->d_sslot,   c->d_stamps};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   for (hipEvent_t e : c->ev) (void)hipEventDestroy(e);
@@ -930,9 +952,11 @@ void free_ctx(phy_ctx* c) {
   delete c;
 }
 
-// Build the traversal program (see DESIGN.md "Traversal program").
-int build_program(int S, const int32_t* peel, int rooted, std::vector<int>& prog, int& nslots,
-                  int& depth) {
+// Build the traversal program (see DESIGN.md "Traversal program"):
+// post-order with the child needing the deeper stack first, every stored
+// moved partial in a slot, every branch matrix numbered in order of use.
+int build_program(int S, const int32_t* peel, int rooted, std::vector<int>& prog,
+                  std::vector<int>& mat_branch, int& nslots, int& depth) {
   const int N = 2 * S - 1;
   std::vector<int> ch1(N, -1), ch2(N, -1);
   std::vector<int> seen(N, 0);
@@ -959,6 +983,7 @@ int build_program(int S, const int32_t* peel, int rooted, std::vector<int>& prog
     if (merged != 2 * S - 3)
       return fail(PHY_EINVAL,
                   "unrooted peel: last row child2 must be node 2S-3 (phylostan.py:264-267)");
+    if (merged < S) return fail(PHY_EINVAL, "unrooted peel: node 2S-3 must be internal");
   }
   // stack need per subtree; larger-need child first (Strahler order)
   std::vector<int> need(N, 0), first(N, -1), second(N, -1);
@@ -993,7 +1018,6 @@ int build_program(int S, const int32_t* peel, int rooted, std::vector<int>& prog
       }
     }
   }
-  // emit post-order with the chosen child order
   std::vector<int> steps;
   {
     std::vector<std::pair<int, int>> st{{root, 0}};
@@ -1018,17 +1042,30 @@ int build_program(int S, const int32_t* peel, int rooted, std::vector<int>& prog
   for (int s = 0; s < S - 1; ++s)
     if (steps[s] != root) slot[steps[s]] = s;
   nslots = S - 2;
-  prog.assign((size_t)(S - 1) * STEP_INTS, 0);
+  prog.assign((size_t)(S - 1) * STEP_INTS, -1);
+  mat_branch.clear();
   for (int s = 0; s < S - 1; ++s) {
     const int v = steps[s];
     const int x = first[v], y = second[v];
     int* p = &prog[(size_t)s * STEP_INTS];
     p[0] = x < S ? x : -(slot[x] + 1);
     p[1] = y < S ? y : -(slot[y] + 1);
-    p[2] = (x == merged) ? -1 : x;
-    p[3] = (y == merged) ? -1 : y;
-    p[4] = (v == root) ? -1 : slot[v];
-    p[5] = v;
+    p[2] = p[3] = p[4] = -1;
+    if (x < S) {  // tip children: their matrices are used at this step
+      p[2] = (int)mat_branch.size();
+      mat_branch.push_back(x);
+    }
+    if (y < S) {
+      p[3] = (int)mat_branch.size();
+      mat_branch.push_back(y);
+    }
+    if (v != root) {  // the step's own branch (identity for the merged one)
+      p[4] = (int)mat_branch.size();
+      mat_branch.push_back(v == merged ? -1 : v);
+    }
+    p[5] = (v == root) ? -1 : slot[v];
+    p[6] = (v != root && v != merged) ? 1 : 0;
+    p[7] = v;
   }
   // simulate both passes to size the LDS stack exactly
   int sp = 0, mx = 0;
@@ -1037,7 +1074,7 @@ int build_program(int S, const int32_t* peel, int rooted, std::vector<int>& prog
     if (p[1] < 0) --sp;
     if (p[0] < 0) --sp;
     if (sp < 0) return fail(PHY_EINVAL, "internal: forward stack underflow");
-    if (p[4] >= 0) mx = std::max(mx, ++sp);
+    if (p[5] >= 0) mx = std::max(mx, ++sp);
   }
   if (sp != 0) return fail(PHY_EINVAL, "internal: forward stack not empty");
   for (int s = S - 2; s >= 0; --s) {
@@ -1062,41 +1099,60 @@ int dalloc(T** p, size_t n) {
   return PHY_OK;
 }
 
-// LDS plan of one sweep launch: how many program steps of P-matrices (and
-// matching dL/dP accumulators) one LDS chunk holds.
-struct LdsPlan {
-  int cs;
-  size_t bytes;
-};
+constexpr size_t LDS_CAP = 160 * 1024;
 
-LdsPlan plan_lds(const phy_ctx* c) {
-  const size_t cap = 160 * 1024;
-  const size_t budget = std::min<size_t>(cap, (size_t)c->lds_budget);
-  int cs = c->nsteps;
-  while (cs > 1 && lds_bytes(c->S, c->C, c->depth, cs) > budget) --cs;
-  LdsPlan p;
-  p.cs = cs;
-  p.bytes = lds_bytes(c->S, c->C, c->depth, cs);
-  return p;
+// Matrices per LDS chunk for the context's budget (>= 3: one step uses up
+// to three) and the chunk boundaries over the program.
+int plan_chunks(phy_ctx* c) {
+  const size_t budget = std::min<size_t>(LDS_CAP, (size_t)c->lds_budget);
+  int cap = c->nmat;
+  while (cap > 3 && lds_bytes(c->S, c->C, c->depth, cap) > budget) --cap;
+  if (lds_bytes(c->S, c->C, c->depth, cap) > LDS_CAP) return fail(PHY_EINVAL, "tree too deep for LDS");
+  if (cap == c->cap_m && c->d_chunk_of) return PHY_OK;
+  std::vector<int> chunk_of(c->nsteps), m0{0};
+  int used = 0, ch = 0;
+  for (int s = 0; s < c->nsteps; ++s) {
+    const int* p = &c->prog[(size_t)s * STEP_INTS];
+    const int n = (p[2] >= 0) + (p[3] >= 0) + (p[4] >= 0);
+    if (used + n > cap) {
+      m0.push_back(m0.back() + used);
+      used = 0;
+      ++ch;
+    }
+    chunk_of[s] = ch;
+    used += n;
+  }
+  m0.push_back(m0.back() + used);
+  if (m0.back() != c->nmat) return fail(PHY_EINVAL, "internal: chunk plan does not cover the matrices");
+  if (c->d_chunk_of) (void)hipFree(c->d_chunk_of);
+  if (c->d_chunk_m0) (void)hipFree(c->d_chunk_m0);
+  c->d_chunk_of = nullptr;
+  c->d_chunk_m0 = nullptr;
+  int rc = dalloc(&c->d_chunk_of, chunk_of.size());
+  if (!rc) rc = dalloc(&c->d_chunk_m0, m0.size());
+  if (rc) return rc;
+  HIP_TRY(hipMemcpy(c->d_chunk_of, chunk_of.data(), chunk_of.size() * sizeof(int), hipMemcpyHostToDevice));
+  HIP_TRY(hipMemcpy(c->d_chunk_m0, m0.data(), m0.size() * sizeof(int), hipMemcpyHostToDevice));
+  c->cap_m = cap;
+  c->nchunks = ch + 1;
+  return PHY_OK;
 }
 
 int launch(phy_ctx* ctx, int n, const double* d_blens, const double* d_model, double* d_out,
            double* d_site, hipStream_t st) {
   const int C = ctx->C, B = ctx->B;
   {
-    PmatArgs pa{d_model, d_blens, ctx->d_gpos, ctx->d_pprog, ctx->d_qp, C, B, ctx->kind, ctx->nsteps,
-                ctx->merged_pos};
+    PmatArgs pa{d_model, d_blens, ctx->d_mat_branch, ctx->d_pmat, ctx->d_qp, C, B, ctx->kind, ctx->nmat};
     hipLaunchKernelGGL(pmat_kernel, dim3(n), dim3(256), 0, st, pa);
     HIP_TRY(hipGetLastError());
   }
   const int gx = std::max(1, std::min(ctx->nblk, (ctx->wg_budget + n - 1) / n));
   if ((size_t)gx * n > (size_t)ctx->wg_cap) return fail(PHY_ERANGE, "workgroup cap exceeded");
-  const LdsPlan plan = plan_lds(ctx);
-  const size_t lds = plan.bytes;
-  SweepArgs sa{ctx->d_tips,  ctx->d_w,      ctx->d_pprog, d_model,     ctx->d_scratch,
-               ctx->d_gslot, ctx->d_sslot,  d_site,       ctx->d_stamps, ctx->S,      ctx->P,
-               ctx->Ppad,    C,             ctx->nsteps,  ctx->nslots, ctx->nblk,
-               ctx->depth,   plan.cs};
+  const size_t lds = lds_bytes(ctx->S, C, ctx->depth, ctx->cap_m);
+  SweepArgs sa{ctx->d_tips,  ctx->d_w,    ctx->d_pmat,   d_model,     ctx->d_scratch, ctx->d_gslot,
+               ctx->d_sslot, d_site,      ctx->d_stamps, ctx->S,      ctx->P,         ctx->Ppad,
+               C,            ctx->nsteps, ctx->nslots,   ctx->nblk,   ctx->depth,     ctx->nmat,
+               ctx->cap_m};
   hipEvent_t e0 = nullptr, e1 = nullptr;
   if (ctx->timing) {
     if (ctx->ev_used + 2 > (int)ctx->ev.size()) {
@@ -1117,15 +1173,18 @@ int launch(phy_ctx* ctx, int n, const double* d_blens, const double* d_model, do
   }
   const int threads = C * WAVE;
   if (threads <= 256)
-    hipLaunchKernelGGL((sweep_kernel<256>), dim3(gx, n), dim3(threads), lds, st, sa, ctx->d_prog);
+    hipLaunchKernelGGL((sweep_kernel<256>), dim3(gx, n), dim3(threads), lds, st, sa, ctx->d_prog,
+                       ctx->d_chunk_of, ctx->d_chunk_m0);
   else if (threads <= 512)
-    hipLaunchKernelGGL((sweep_kernel<512>), dim3(gx, n), dim3(threads), lds, st, sa, ctx->d_prog);
+    hipLaunchKernelGGL((sweep_kernel<512>), dim3(gx, n), dim3(threads), lds, st, sa, ctx->d_prog,
+                       ctx->d_chunk_of, ctx->d_chunk_m0);
   else
-    hipLaunchKernelGGL((sweep_kernel<1024>), dim3(gx, n), dim3(threads), lds, st, sa, ctx->d_prog);
+    hipLaunchKernelGGL((sweep_kernel<1024>), dim3(gx, n), dim3(threads), lds, st, sa, ctx->d_prog,
+                       ctx->d_chunk_of, ctx->d_chunk_m0);
   HIP_TRY(hipGetLastError());
   if (ctx->timing) HIP_TRY(hipEventRecord(e1, st));
   FinArgs fa{ctx->d_gslot, ctx->d_sslot, ctx->d_qp, d_blens, d_model, ctx->d_gpos, d_out,
-             C,            B,            ctx->nsteps, gx, phy_output_len(ctx)};
+             C,            B,            ctx->nmat, gx, phy_output_len(ctx)};
   hipLaunchKernelGGL(finalize_g_kernel, dim3((C * B * 16 + 63) / 64, n), dim3(256), 0, st, fa);
   HIP_TRY(hipGetLastError());
   hipLaunchKernelGGL(finalize_s_kernel, dim3(n), dim3(256), ((size_t)C * B + B + 256) * sizeof(double), st,
@@ -1170,41 +1229,35 @@ int phy_create(int S, int P, int C, int rooted, int model, const uint8_t* tipcod
   c->nblk = (P + WAVE - 1) / WAVE;
   c->Ppad = c->nblk * WAVE;
   c->stream = nullptr;
-  std::vector<int> prog;
-  int rc = build_program(S, peel, c->rooted, prog, c->nslots, c->depth);
+  std::vector<int> mat_branch;
+  int rc = build_program(S, peel, c->rooted, c->prog, mat_branch, c->nslots, c->depth);
   if (rc) {
     delete c;
     return rc;
   }
   c->nsteps = S - 1;
+  c->nmat = (int)mat_branch.size();
   c->g_mode = 0;
   {
     const char* lb = getenv("PHY_LDS_BUDGET");
-    c->lds_budget = lb ? std::max(16384, atoi(lb)) : 160 * 1024;
+    c->lds_budget = lb ? std::max(16384, atoi(lb)) : 80 * 1024;
     const char* env = getenv("PHY_WG_BUDGET");
     c->wg_budget = env ? std::max(1, atoi(env)) : 512;
-    const char* gm = getenv("PHY_G_MODE");
-    if (gm) c->g_mode = atoi(gm);
   }
-  c->wg_cap = std::min<long>((long)c->nblk * max_draws, (long)c->wg_budget + max_draws);
+  c->wg_cap = (int)std::min<long>((long)c->nblk * max_draws, (long)c->wg_budget + max_draws);
   hipError_t he = hipSetDevice(device);
   if (he != hipSuccess) {
     delete c;
     return fail(PHY_EHIP, std::string("hipSetDevice: ") + hipGetErrorString(he));
   }
-  int lds_max = 0;
-  (void)hipDeviceGetAttribute(&lds_max, hipDeviceAttributeMaxSharedMemoryPerBlock, device);
   // gfx950: one workgroup may use the whole 160 KiB LDS; dynamic LDS above
   // 64 KiB has to be opted into per kernel.
-  c->max_lds = 65536;
   {
-    const int cap = 160 * 1024;
     const void* ks[] = {(const void*)sweep_kernel<256>, (const void*)sweep_kernel<512>,
                         (const void*)sweep_kernel<1024>};
-    for (const void* k : ks) (void)hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, cap);
-    lds_max = std::max(lds_max, cap);
+    for (const void* k : ks) (void)hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)LDS_CAP);
   }
-  if (lds_bytes(S, C, c->depth, 1) > (size_t)lds_max) {
+  if (lds_bytes(S, C, c->depth, 3) > LDS_CAP) {
     delete c;
     return fail(PHY_EINVAL, "tree too deep for the LDS stack");
   }
@@ -1230,45 +1283,40 @@ int phy_create(int S, int P, int C, int rooted, int model, const uint8_t* tipcod
   const size_t ncolwg = (size_t)C * WAVE;
   TRY_C(dalloc(&c->d_tips, (size_t)S * c->Ppad));
   TRY_C(dalloc(&c->d_w, (size_t)c->Ppad));
-  TRY_C(dalloc(&c->d_prog, prog.size()));
-  TRY_C(dalloc(&c->d_pprog, (size_t)max_draws * C * c->nsteps * 32));
+  TRY_C(dalloc(&c->d_prog, c->prog.size()));
+  TRY_C(dalloc(&c->d_mat_branch, (size_t)c->nmat));
+  TRY_C(dalloc(&c->d_gpos, (size_t)c->B));
+  TRY_C(dalloc(&c->d_pmat, (size_t)max_draws * C * c->nmat * 16));
   TRY_C(dalloc(&c->d_qp, (size_t)max_draws * C * c->B * 16));
   TRY_C(dalloc(&c->d_model, (size_t)max_draws * (10 + 2 * C)));
   TRY_C(dalloc(&c->d_blens, (size_t)max_draws * c->B));
   TRY_C(dalloc(&c->d_out, (size_t)max_draws * phy_output_len(c)));
   TRY_C(dalloc(&c->d_site, (size_t)max_draws * P));
   TRY_C(dalloc(&c->d_scratch, (size_t)c->wg_cap * std::max(c->nslots, 1) * 2 * ncolwg));
-  TRY_C(dalloc(&c->d_gslot, (size_t)c->wg_cap * C * c->nsteps * 32));
-  TRY_C(dalloc(&c->d_gpos, (size_t)c->B));
+  TRY_C(dalloc(&c->d_gslot, (size_t)c->wg_cap * C * c->nmat * 16));
   TRY_C(dalloc(&c->d_sslot, (size_t)c->wg_cap * C * 8));
   if (PHY_STAMP) TRY_C(dalloc(&c->d_stamps, (size_t)c->wg_cap * C * 8));
   {
     std::vector<uint8_t> tips((size_t)S * c->Ppad, 15);
-    for (int t = 0; t < S; ++t)
-      std::memcpy(&tips[(size_t)t * c->Ppad], tipcodes + (size_t)t * P, P);
+    for (int t = 0; t < S; ++t) std::memcpy(&tips[(size_t)t * c->Ppad], tipcodes + (size_t)t * P, P);
     std::vector<double> w(c->Ppad, 0.0);
     std::memcpy(w.data(), weights, sizeof(double) * P);
-    HIP_C(hipMemcpy(c->d_tips, tips.data(), tips.size(), hipMemcpyHostToDevice));
-    HIP_C(hipMemcpy(c->d_w, w.data(), w.size() * sizeof(double), hipMemcpyHostToDevice));
-    HIP_C(hipMemcpy(c->d_prog, prog.data(), prog.size() * sizeof(int), hipMemcpyHostToDevice));
     std::vector<int> gpos(c->B, -1);
-    for (int st = 0; st < c->nsteps; ++st)
-      for (int w = 0; w < 2; ++w) {
-        const int b = prog[(size_t)st * STEP_INTS + 2 + w];
-        if (b >= 0) gpos[b] = st * 2 + w;
-      }
-    c->merged_pos = -1;
-    for (int st = 0; st < c->nsteps; ++st)
-      for (int w = 0; w < 2; ++w)
-        if (prog[(size_t)st * STEP_INTS + 2 + w] < 0) c->merged_pos = st * 2 + w;
+    for (int m = 0; m < c->nmat; ++m)
+      if (mat_branch[m] >= 0) gpos[mat_branch[m]] = m;
     for (int b = 0; b < c->B; ++b)
       if (gpos[b] < 0) {
         std::string m_ = "internal: branch " + std::to_string(b) + " not in the program";
         free_ctx(c);
         return fail(PHY_EINVAL, m_);
       }
+    HIP_C(hipMemcpy(c->d_tips, tips.data(), tips.size(), hipMemcpyHostToDevice));
+    HIP_C(hipMemcpy(c->d_w, w.data(), w.size() * sizeof(double), hipMemcpyHostToDevice));
+    HIP_C(hipMemcpy(c->d_prog, c->prog.data(), c->prog.size() * sizeof(int), hipMemcpyHostToDevice));
+    HIP_C(hipMemcpy(c->d_mat_branch, mat_branch.data(), mat_branch.size() * sizeof(int), hipMemcpyHostToDevice));
     HIP_C(hipMemcpy(c->d_gpos, gpos.data(), gpos.size() * sizeof(int), hipMemcpyHostToDevice));
   }
+  TRY_C(plan_chunks(c));
   *out = c;
   return PHY_OK;
 }
@@ -1311,18 +1359,14 @@ int phy_eval(phy_ctx* ctx, int n_draws, const double* blens, const double* model
   HIP_TRY(hipSetDevice(ctx->device));
   hipStream_t st = ctx->stream;
   const int ml = 10 + 2 * ctx->C;
-  HIP_TRY(hipMemcpyAsync(ctx->d_blens, blens, sizeof(double) * n_draws * ctx->B,
-                         hipMemcpyHostToDevice, st));
-  HIP_TRY(hipMemcpyAsync(ctx->d_model, model, sizeof(double) * n_draws * ml,
-                         hipMemcpyHostToDevice, st));
-  int rc = launch(ctx, n_draws, ctx->d_blens, ctx->d_model, ctx->d_out,
-                  site_ll ? ctx->d_site : nullptr, st);
+  HIP_TRY(hipMemcpyAsync(ctx->d_blens, blens, sizeof(double) * n_draws * ctx->B, hipMemcpyHostToDevice, st));
+  HIP_TRY(hipMemcpyAsync(ctx->d_model, model, sizeof(double) * n_draws * ml, hipMemcpyHostToDevice, st));
+  int rc = launch(ctx, n_draws, ctx->d_blens, ctx->d_model, ctx->d_out, site_ll ? ctx->d_site : nullptr, st);
   if (rc) return rc;
-  HIP_TRY(hipMemcpyAsync(out, ctx->d_out, sizeof(double) * n_draws * phy_output_len(ctx),
-                         hipMemcpyDeviceToHost, st));
+  HIP_TRY(hipMemcpyAsync(out, ctx->d_out, sizeof(double) * n_draws * phy_output_len(ctx), hipMemcpyDeviceToHost,
+                         st));
   if (site_ll)
-    HIP_TRY(hipMemcpyAsync(site_ll, ctx->d_site, sizeof(double) * n_draws * ctx->P,
-                           hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipMemcpyAsync(site_ll, ctx->d_site, sizeof(double) * n_draws * ctx->P, hipMemcpyDeviceToHost, st));
   HIP_TRY(hipStreamSynchronize(st));
   return PHY_OK;
 }
@@ -1384,8 +1428,12 @@ int phy_set_tuning(phy_ctx* ctx, int wg_budget, int g_mode, int lds_budget) {
     ctx->wg_budget = wg_budget;
   }
   if (g_mode < 0 || g_mode > 2) return fail(PHY_EINVAL, "g_mode must be 0, 1 or 2");
-  ctx->g_mode = g_mode;
-  if (lds_budget > 0) ctx->lds_budget = std::max(16384, std::min(lds_budget, 160 * 1024));
+  ctx->g_mode = g_mode;  // dL/dP always accumulates in LDS chunks (kept for ABI stability)
+  if (lds_budget > 0) {
+    ctx->lds_budget = std::max(16384, std::min(lds_budget, (int)LDS_CAP));
+    HIP_TRY(hipSetDevice(ctx->device));
+    return plan_chunks(ctx);
+  }
   return PHY_OK;
 }
 
@@ -1402,10 +1450,9 @@ int phy_debug_stamps(phy_ctx* ctx, unsigned long long* out, int n) {
 
 int phy_lds_plan(const phy_ctx* ctx, int* g_in_lds, int* chunk_steps, int* lds_bytes_out) {
   if (!ctx) return fail(PHY_EINVAL, "NULL ctx");
-  const LdsPlan p = plan_lds(ctx);
-  if (g_in_lds) *g_in_lds = 1;
-  if (chunk_steps) *chunk_steps = p.cs;
-  if (lds_bytes_out) *lds_bytes_out = (int)p.bytes;
+  if (g_in_lds) *g_in_lds = ctx->nchunks;  // number of P / dL/dP chunks per pass
+  if (chunk_steps) *chunk_steps = ctx->cap_m;
+  if (lds_bytes_out) *lds_bytes_out = (int)lds_bytes(ctx->S, ctx->C, ctx->depth, ctx->cap_m);
   return PHY_OK;
 }
 

@@ -162,7 +162,7 @@ class TreeLikelihood:
     def lds_plan(self):
         vals = [ctypes.c_int() for _ in range(3)]
         _lib.check(self.lib.phy_lds_plan(self.ctx, *[ctypes.byref(v) for v in vals]), "phy_lds_plan")
-        return dict(zip(("g_in_lds", "chunk_steps", "lds_bytes"), [v.value for v in vals]))
+        return dict(zip(("n_chunks", "matrices_per_chunk", "lds_bytes"), [v.value for v in vals]))
 
     def timing_start(self):
         _lib.check(self.lib.phy_timing_start(self.ctx), "phy_timing_start")

@@ -82,15 +82,19 @@ def test_all_ambiguous_and_padding():
     check_case(case)
 
 
-@pytest.mark.parametrize("g_mode,lds_budget", [(1, 0), (2, 0), (2, 40000), (0, 24000), (1, 24000)])
-def test_lds_plans(g_mode, lds_budget):
-    """dL/dP in LDS / global, whole-program and chunked P-matrix staging."""
+@pytest.mark.parametrize("lds_budget,chunks", [(160 * 1024, 2), (80 * 1024, 3), (40000, None),
+                                               (24000, None)])
+def test_lds_plans(lds_budget, chunks):
+    """Whole-program and chunked staging of P-matrices / dL/dP in LDS."""
     case = cases.fluA_case()
     eng = _engine(case)
-    eng.set_tuning(0, g_mode, lds_budget)
+    eng.set_tuning(0, 0, lds_budget)
     plan = eng.lds_plan()
-    if lds_budget:
-        assert plan["chunk_steps"] < case.S - 1
+    if chunks is not None:
+        assert plan["n_chunks"] <= chunks
+    else:
+        assert plan["n_chunks"] > 1
+    assert plan["lds_bytes"] <= lds_budget
     check_case(case, eng)
 
 
@@ -112,11 +116,20 @@ def test_batched_draws_match_single():
         check_case(c, eng, res[k])
 
 
-def test_persistent_workgroups_loop():
-    """Fewer workgroups than pattern blocks: every workgroup loops."""
+@pytest.mark.parametrize("lds_budget", [0, 30000])
+def test_persistent_workgroups_loop(lds_budget):
+    """Fewer workgroups than pattern blocks: every workgroup loops (with the
+    whole program or several chunks resident)."""
     case = cases.random_case(21, S=20, P=64 * 9 + 5, C=3)
     eng = _engine(case)
-    eng.set_tuning(2, 0)
+    eng.set_tuning(2, 0, lds_budget)
+    check_case(case, eng)
+
+
+def test_single_chunk_resident_for_small_tree():
+    case = cases.random_case(22, S=10, P=300, C=2, model="HKY")
+    eng = _engine(case)
+    assert eng.lds_plan()["n_chunks"] == 1
     check_case(case, eng)
 
 
