@@ -1,8 +1,8 @@
 """Diagnostic: per-phase cycle split of the sweep kernel (stamp build)."""
 import ctypes, os, sys
 import numpy as np
-os.environ["PHYLO_HIP_LIB"] = os.path.join(os.path.dirname(os.path.abspath(__file__)), "phylostan_amd", "libphylo_hip_stamp.so")
-sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+os.environ["PHYLO_HIP_LIB"] = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "phylostan_amd", "libphylo_hip_stamp.so")
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from phylostan_amd.engine import TreeLikelihood
 from phylostan_amd import _lib
 from tests import cases
