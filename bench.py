@@ -51,7 +51,7 @@ def parse():
     ap.add_argument("--single-eval", action="store_true",
                     help="also time unbatched (draws=1) evaluations and report them")
     ap.add_argument("--wg-budget", type=int, default=0)
-    ap.add_argument("--g-mode", type=int, default=0)
+    ap.add_argument("--cols", type=int, default=0, help="pattern columns per lane (0 = automatic)")
     ap.add_argument("--lds-budget", type=int, default=0)
     ap.add_argument("--json-out", default=None)
     return ap.parse_args()
@@ -158,8 +158,8 @@ def main():
     sl = ShardedLikelihood(prob["tipcodes"], prob["weights"], prob["peel0"], prob["rooted"], prob["model"],
                            C, shard_rank, shard_world, device=local, max_draws=draws)
     eng = sl.engine
-    if args.wg_budget or args.g_mode or args.lds_budget:
-        eng.set_tuning(args.wg_budget, args.g_mode, args.lds_budget)
+    if args.wg_budget or args.cols or args.lds_budget:
+        eng.set_tuning(args.wg_budget, args.cols, args.lds_budget)
     info = eng.program_info()
     info.update(eng.lds_plan())
     B = eng.B

@@ -126,15 +126,23 @@ int phy_sync(phy_ctx* ctx);
 int phy_timing_start(phy_ctx* ctx);
 int phy_timing_read(phy_ctx* ctx, double* total_ms, int* launches);
 
-/* Tuning: persistent workgroup budget per launch (0 = keep), g_mode
- * (reserved, must be 0..2) and the LDS bytes one workgroup may use (0 =
- * keep; default 80 KiB = two workgroups per CU; smaller budgets stage the
- * P-matrices and dL/dP accumulators in more chunks). */
-int phy_set_tuning(phy_ctx* ctx, int wg_budget, int g_mode, int lds_budget);
+/* Tuning: persistent workgroup budget per launch (0 = keep), columns per
+ * lane `cols` (0 = automatic, 1 or 2) and the LDS bytes one workgroup may
+ * use (0 = keep; smaller budgets stage the P-matrices and dL/dP
+ * accumulators in more chunks).  The automatic plan (no PHY_LDS_BUDGET, no
+ * PHY_COLS, nothing set here) takes the first of: two columns at 80 KiB
+ * (two workgroups per CU), two columns at 160 KiB, one column at 80 KiB
+ * that keeps LDS chunks of >= 24 matrices.  The environment variables
+ * PHY_WG_BUDGET, PHY_COLS and PHY_LDS_BUDGET set the defaults at
+ * phy_create. */
+int phy_set_tuning(phy_ctx* ctx, int wg_budget, int cols, int lds_budget);
 
 /* The LDS plan the next launch will use: chunks per pass, matrices per
  * chunk, LDS bytes per workgroup. */
 int phy_lds_plan(const phy_ctx* ctx, int* n_chunks, int* matrices_per_chunk, int* lds_bytes);
+
+/* Pattern columns each lane carries in the current plan (1 or 2). */
+int phy_columns_per_lane(const phy_ctx* ctx);
 
 /* Diagnostic builds only (-DPHY_STAMP=1): per-wave s_memtime stamps of the
  * last launch, [wg][C][8] = start, forward, root, reverse, end of first

@@ -40,6 +40,7 @@ SIGNATURES = {
     "phy_timing_read": (ctypes.c_int, [ctypes.c_void_p, _c_double_p, _c_int_p]),
     "phy_set_tuning": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int]),
     "phy_lds_plan": (ctypes.c_int, [ctypes.c_void_p, _c_int_p, _c_int_p, _c_int_p]),
+    "phy_columns_per_lane": (ctypes.c_int, [ctypes.c_void_p]),
 }
 
 

@@ -155,14 +155,18 @@ class TreeLikelihood:
     def sync(self):
         _lib.check(self.lib.phy_sync(self.ctx), "phy_sync")
 
-    def set_tuning(self, wg_budget=0, g_mode=0, lds_budget=0):
-        _lib.check(self.lib.phy_set_tuning(self.ctx, int(wg_budget), int(g_mode), int(lds_budget)),
+    def set_tuning(self, wg_budget=0, cols=0, lds_budget=0):
+        """Persistent-workgroup budget, columns per lane (0 = automatic, 1, 2)
+        and LDS bytes per workgroup (0 = keep); see include/phylo_hip.h."""
+        _lib.check(self.lib.phy_set_tuning(self.ctx, int(wg_budget), int(cols), int(lds_budget)),
                    "phy_set_tuning")
 
     def lds_plan(self):
         vals = [ctypes.c_int() for _ in range(3)]
         _lib.check(self.lib.phy_lds_plan(self.ctx, *[ctypes.byref(v) for v in vals]), "phy_lds_plan")
-        return dict(zip(("n_chunks", "matrices_per_chunk", "lds_bytes"), [v.value for v in vals]))
+        out = dict(zip(("n_chunks", "matrices_per_chunk", "lds_bytes"), [v.value for v in vals]))
+        out["cols"] = self.lib.phy_columns_per_lane(self.ctx)
+        return out
 
     def timing_start(self):
         _lib.check(self.lib.phy_timing_start(self.ctx), "phy_timing_start")

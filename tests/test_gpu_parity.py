@@ -82,7 +82,7 @@ def test_all_ambiguous_and_padding():
     check_case(case)
 
 
-@pytest.mark.parametrize("lds_budget,chunks", [(160 * 1024, 2), (80 * 1024, 3), (40000, None),
+@pytest.mark.parametrize("lds_budget,chunks", [(160 * 1024, 2), (80 * 1024, 4), (40000, None),
                                                (24000, None)])
 def test_lds_plans(lds_budget, chunks):
     """Whole-program and chunked staging of P-matrices / dL/dP in LDS."""
@@ -99,11 +99,33 @@ def test_lds_plans(lds_budget, chunks):
     check_case(case, eng)
 
 
-def test_batched_draws_match_single():
+@pytest.mark.parametrize("cols", [1, 2])
+@pytest.mark.parametrize("seed,S,P,C,model,rooted,cat,lds", [
+    (31, 12, 130, 4, "HKY", True, False, 0),       # ragged: 130 = 128 + 2
+    (32, 17, 257, 5, "GTR", False, False, 0),      # unrooted, odd C
+    (33, 40, 300, 2, "GTR", True, True, 0),        # caterpillar
+    (34, 64, 700, 4, "GTR", True, False, 40000),   # chunked, persistent loop
+    (35, 9, 100, 8, "JC69", True, False, 0),       # 512-thread workgroups
+])
+def test_columns_per_lane(cols, seed, S, P, C, model, rooted, cat, lds):
+    """One and two pattern columns per lane give the oracle's answers."""
+    case = cases.random_case(seed, S=S, P=P, C=C, model=model, rooted=rooted, caterpillar=cat)
+    eng = _engine(case)
+    eng.set_tuning(3 if lds else 0, cols, lds or 160 * 1024)
+    assert eng.lds_plan()["cols"] == cols
+    check_case(case, eng)
+
+
+@pytest.mark.parametrize("wg_budget", [0, 7])
+def test_batched_draws_match_single(wg_budget):
+    """Batched draws; wg_budget 7 = one workgroup per draw, whose dL/dP goes
+    straight to the output rows across chunk flushes (no finalize sum)."""
     base = cases.fluA_case()
     rng = np.random.default_rng(3)
     n = 7
     eng = _engine(base, max_draws=n)
+    if wg_budget:
+        eng.set_tuning(wg_budget, 0, 0)
     blens = base.blens[None, :] * rng.uniform(0.5, 1.5, (n, 1))
     mvs = []
     for k in range(n):

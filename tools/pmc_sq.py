@@ -1,0 +1,46 @@
+#!/usr/bin/env python
+"""Collect SQ / TCC counters of the sweep kernel in separate rocprofv3 --pmc
+passes (kernel-trace only) and print per-dispatch averages.  Run on the GPU
+box:  python tools/pmc_sq.py [bench.py args ...]"""
+import csv
+import glob
+import json
+import os
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+PASSES = [
+    "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU",
+    "SQ_INSTS_LDS SQ_INSTS_SALU SQ_INSTS_SMEM SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_ACTIVE_INST_LDS SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT",
+    "SQ_INSTS_VALU_FMA_F64 SQ_INSTS_VALU_MUL_F64 SQ_INSTS_VALU_ADD_F64 SQ_INSTS_BRANCH SQ_ACTIVE_INST_SCA SQ_ACTIVE_INST_VMEM SQ_INST_CYCLES_VMEM_RD SQ_INSTS",
+    "GRBM_GUI_ACTIVE TCC_HIT_sum TCC_MISS_sum TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_DRAM_sum TCC_EA0_WRREQ_sum",
+]
+
+
+def main():
+    bench_args = sys.argv[1:] or ["--steps", "3", "--warmup", "1", "--no-cpu-baseline"]
+    out = {}
+    for k, counters in enumerate(PASSES):
+        d = os.path.join(ROOT, "gpurun_out", "pmc_sq", "p%d" % k)
+        cmd = ["rocprofv3", "--kernel-trace", "-d", d, "-o", "run", "--output-format", "csv"]
+        cmd += ["--pmc"] + counters.split()
+        cmd += ["--", sys.executable, os.path.join(ROOT, "bench.py")] + bench_args
+        r = subprocess.run(cmd, stdout=subprocess.DEVNULL, stderr=subprocess.PIPE, timeout=900,
+                           env=dict(os.environ, TMPDIR="/tmp"))
+        if r.returncode != 0:
+            print("pass %d failed: %s" % (k, r.stderr.decode()[-2000:]), file=sys.stderr)
+            continue
+        acc = {}
+        for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
+            for row in csv.DictReader(open(f)):
+                if "sweep_kernel" not in row["Kernel_Name"]:
+                    continue
+                acc.setdefault(row["Counter_Name"], []).append(float(row["Counter_Value"]))
+        for cn, v in acc.items():
+            out[cn] = sum(v) / len(v)
+    print(json.dumps(out, indent=1))
+
+
+if __name__ == "__main__":
+    main()
