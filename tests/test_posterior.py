@@ -1,0 +1,283 @@
+"""Host posterior (phylostan_amd/posterior.py): value and gradient.
+
+The likelihood underneath is the numpy oracle stand-in (CPU); the gradient
+of the whole log density -- transforms, priors, height reparametrisation,
+chain rule through the eigendecomposition -- is checked against central
+finite differences of the value, for every model option the posterior
+supports.  Values of the pieces that restate Stan functions are checked
+against literal loop restatements of the emitted Stan code
+(generate_script.py:285-349, :352-419, :606-619, :711-752).
+"""
+import math
+
+import numpy as np
+import pytest
+
+from phylostan_amd import models, priors
+from phylostan_amd.posterior import ModelSpec, Posterior, TreeData
+from phylostan_amd.transforms import Lower, Simplex, Unit
+from tests import cases
+from tests.oracle_backend import OracleLikelihood
+
+
+def preorder_map(peel0):
+    """utils.get_preorder for a 0-based peel: 1-based [node, parent] rows."""
+    peel0 = np.asarray(peel0)
+    kids = {int(v): (int(a), int(b)) for a, b, v in peel0}
+    root = int(peel0[-1, 2])
+    rows = [[root + 1, 0]]
+    order = []
+    stack = [root]
+    while stack:
+        v = stack.pop()
+        order.append(v)
+        if v in kids:
+            a, b = kids[v]
+            stack.append(b)
+            stack.append(a)
+    par = {}
+    for v, (a, b) in kids.items():
+        par[a] = v
+        par[b] = v
+    rows += [[v + 1, par[v] + 1] for v in order[1:]]
+    return np.array(rows)
+
+
+def lowers_for(peel0, tip_dates):
+    S = len(tip_dates)
+    low = np.zeros(2 * S - 1)
+    low[:S] = tip_dates
+    for a, b, v in np.asarray(peel0):
+        low[v] = max(low[a], low[b])
+    return low
+
+
+def fd_grad(post, u, h=1e-5):
+    g = np.empty_like(u)
+    for i in range(len(u)):
+        e = np.zeros_like(u)
+        e[i] = h
+        g[i] = (post.log_prob((u + e)[None])[0] - post.log_prob((u - e)[None])[0]) / (2 * h)
+    return g
+
+
+def check_grad(post, u, tol=2e-6):
+    lp, G = post.log_prob_grad(u[None])
+    assert np.isfinite(lp[0])
+    fd = fd_grad(post, u)
+    err = np.max(np.abs(G[0] - fd)) / max(1.0, np.max(np.abs(fd)))
+    assert err < tol, "gradient vs FD: %.3e (worst index %d: %r vs %r)" % (
+        err, int(np.argmax(np.abs(G[0] - fd))), G[0][np.argmax(np.abs(G[0] - fd))],
+        fd[np.argmax(np.abs(G[0] - fd))])
+    return lp[0], G[0]
+
+
+# ------------------------------------------------------------- transforms
+@pytest.mark.parametrize("tr", [Lower(0.0, 3), Lower(0.1), Unit(4), Unit(), Simplex(4), Simplex(6)])
+def test_transform_grad_and_inverse(tr):
+    rng = np.random.default_rng(0)
+    u = rng.uniform(-2, 2, (3, tr.size))
+    x, lj, st = tr.constrain(u)
+    np.testing.assert_allclose(tr.unconstrain(x), u, rtol=1e-10, atol=1e-10)
+    w = rng.normal(size=x.shape)
+    g = tr.backward(st, w, 1.0)
+    h = 1e-6
+    for i in range(tr.size):
+        e = np.zeros_like(u)
+        e[:, i] = h
+        xp, ljp, _ = tr.constrain(u + e)
+        xm, ljm, _ = tr.constrain(u - e)
+        fd = ((xp - xm) * w).reshape(3, -1).sum(1) / (2 * h) + (ljp - ljm) / (2 * h)
+        np.testing.assert_allclose(g[:, i], fd, rtol=1e-6, atol=1e-8)
+    if isinstance(tr, Simplex):
+        np.testing.assert_allclose(x.sum(1), 1.0)
+
+
+def test_simplex_matches_stan_stick_breaking():
+    """Stan Math simplex_constrain: z_k = inv_logit(y_k - log(K-k))."""
+    y = np.array([0.3, -1.2, 0.7])
+    K = 4
+    x = np.zeros(K)
+    stick = 1.0
+    for k in range(K - 1):
+        z = 1.0 / (1.0 + math.exp(-(y[k] - math.log(K - (k + 1)))))
+        x[k] = stick * z
+        stick -= x[k]
+    x[K - 1] = stick
+    np.testing.assert_allclose(Simplex(4).constrain(y[None])[0][0], x, rtol=1e-14)
+
+
+# ------------------------------------------------------ Stan restatements
+def _stan_constant_coalescent(times, internal, theta):
+    """Literal loop of generate_script.py:303-342 (0-based)."""
+    idx = sorted(range(len(times)), key=lambda i: times[i])
+    lp, k = 0.0, 0.0
+    start = times[idx[0]]
+    for i in idx:
+        finish = times[i]
+        interval = finish - start
+        if interval != 0.0:
+            lp -= interval * (k * (k - 1.0) / 2.0) / theta
+        if not internal[i]:
+            k += 1.0
+        else:
+            k -= 1.0
+            lp -= math.log(theta)
+        start = finish
+    return lp
+
+
+def _stan_skyride(times, internal, pop):
+    idx = sorted(range(len(times)), key=lambda i: times[i])
+    lp, k, index = 0.0, 0.0, 0
+    start = times[idx[0]]
+    for i in idx:
+        finish = times[i]
+        interval = finish - start
+        if interval != 0.0:
+            lp -= interval * (k * (k - 1.0) / 2.0) / math.exp(pop[index])
+            if internal[i]:
+                lp -= pop[index]
+                index += 1
+        k += -1.0 if internal[i] else 1.0
+        start = finish
+    return lp
+
+
+def _random_times(rng, S, hetero=True):
+    peel = cases.random_peel(S, rng)
+    tips = rng.uniform(0, 2, S) if hetero else np.zeros(S)
+    low = lowers_for(peel, tips)
+    t = np.zeros(2 * S - 1)
+    t[:S] = tips
+    for a, b, v in peel:
+        t[v] = max(t[a], t[b]) + rng.exponential(0.5)
+    internal = np.arange(2 * S - 1) >= S
+    return t, internal, low
+
+
+def test_coalescent_restatements_and_gradients():
+    rng = np.random.default_rng(3)
+    for trial in range(4):
+        S = 9
+        t, internal, _ = _random_times(rng, S, hetero=trial % 2 == 0)
+        theta = rng.uniform(0.5, 3.0)
+        lp, gt, gth = priors.constant_coalescent(t[None], internal, np.array([theta]))
+        assert abs(lp[0] - _stan_constant_coalescent(t, internal, theta)) < 1e-12
+        pop = rng.normal(size=S - 1)
+        lp2, gt2, gp2 = priors.skyride_coalescent(t[None], internal, pop[None])
+        assert abs(lp2[0] - _stan_skyride(t, internal, pop)) < 1e-12
+        h = 1e-6
+        for i in range(S, 2 * S - 1):
+            e = np.zeros_like(t)
+            e[i] = h
+            fd = (_stan_constant_coalescent(t + e, internal, theta) - _stan_constant_coalescent(t - e, internal, theta)) / (2 * h)
+            assert abs(gt[0, i] - fd) < 1e-6
+            fd2 = (_stan_skyride(t + e, internal, pop) - _stan_skyride(t - e, internal, pop)) / (2 * h)
+            assert abs(gt2[0, i] - fd2) < 1e-6
+        fdth = (_stan_constant_coalescent(t, internal, theta + h) - _stan_constant_coalescent(t, internal, theta - h)) / (2 * h)
+        assert abs(gth[0] - fdth) < 1e-6
+        for j in range(S - 1):
+            e = np.zeros_like(pop)
+            e[j] = h
+            fd = (_stan_skyride(t, internal, pop + e) - _stan_skyride(t, internal, pop - e)) / (2 * h)
+            assert abs(gp2[0, j] - fd) < 1e-6
+
+
+def test_skygrid_and_gmrf_gradients():
+    rng = np.random.default_rng(5)
+    S = 8
+    t, internal, _ = _random_times(rng, S)
+    grid = np.linspace(0, t.max() * 0.9, 6)[1:]
+    pop = rng.normal(size=len(grid))
+    lp, gt, gp = priors.skygrid_coalescent(t[None], internal, pop[None], grid)
+    h = 1e-6
+    f = lambda tt, pp: priors.skygrid_coalescent(tt[None], internal, pp[None], grid)[0][0]
+    for i in range(S, 2 * S - 1):
+        e = np.zeros_like(t)
+        e[i] = h
+        assert abs(gt[0, i] - (f(t + e, pop) - f(t - e, pop)) / (2 * h)) < 1e-6
+    for j in range(len(pop)):
+        e = np.zeros_like(pop)
+        e[j] = h
+        assert abs(gp[0, j] - (f(t, pop + e) - f(t, pop - e)) / (2 * h)) < 1e-6
+    tau = np.array([2.5])
+    lpg, gl, gtau = priors.gmrf(pop[None], tau)
+    ref = math.log(2.5) * (len(pop) - 1) / 2 - 2.5 / 2 * np.sum(np.diff(pop) ** 2) - (len(pop) - 1) / 2 * math.log(2 * math.pi)
+    assert abs(lpg[0] - ref) < 1e-12
+
+
+# ------------------------------------------------------- whole posterior
+def _random_posterior(seed, model, C, clock, coalescent=None, invariant=False, hetero=False,
+                      heterogeneity="weibull", S=7, P=40):
+    case = cases.random_case(seed, S=S, P=P, C=1, model=model, rooted=clock is not None)
+    rng = np.random.default_rng(seed)
+    tips = rng.uniform(0, 1.0, S) if hetero else np.zeros(S)
+    tree = TreeData(S, case.peel0, preorder_map(case.peel0), lowers_for(case.peel0, tips) if hetero else None,
+                    float(tips.max()) if hetero else None)
+    spec = ModelSpec(model=model, categories=C, invariant=invariant, heterogeneity=heterogeneity, clock=clock,
+                     estimate_rate=clock is not None, coalescent=coalescent, heterochronous=hetero,
+                     grid=5 if coalescent == "skygrid" else None, cutoff=2.0 if coalescent == "skygrid" else None)
+    lik = OracleLikelihood(case.tipcodes, case.weights, case.peel0, clock is not None, model, spec.C)
+    return Posterior(spec, tree, lik), rng
+
+
+CONFIGS = [
+    dict(model="JC69", C=1, clock=None),
+    dict(model="GTR", C=4, clock=None),
+    dict(model="HKY", C=4, clock="strict", coalescent="constant", hetero=True),
+    dict(model="HKY", C=1, clock="strict", coalescent="constant", invariant=True),
+    dict(model="GTR", C=3, clock="strict", coalescent="skyride"),
+    dict(model="GTR", C=3, clock="strict", coalescent="skygrid", hetero=True, invariant=True),
+    dict(model="JC69", C=3, clock="strict", coalescent=None, heterogeneity="discrete"),
+]
+
+
+@pytest.mark.parametrize("cfg", CONFIGS, ids=lambda c: "-".join(str(v) for v in c.values()))
+def test_posterior_gradient_fd(cfg):
+    post, rng = _random_posterior(11, **cfg)
+    u = rng.uniform(-1.0, 1.0, post.dim)
+    if post.param("rate") is not None:
+        u[post.param("rate").sl] = math.log(0.3)
+    check_grad(post, u)
+
+
+def test_fluA_posterior_at_readme_point():
+    """fluA HKY+W4, strict clock, constant coalescent, heterochronous at the
+    README.md:104-108 means; gradient vs FD and the likelihood term equals
+    the oracle's at the same blens."""
+    d = cases.load_layout("fluA")
+    S = d["tipbits"].shape[0]
+    peel0 = d["peel"] - 1
+    tree = TreeData(S, peel0, d["map"], d["lowers"], float(d["oldest"]))
+    spec = ModelSpec(model="HKY", categories=4, clock="strict", estimate_rate=True, coalescent="constant",
+                     heterochronous=True)
+    lik = OracleLikelihood(d["tipbits"], d["weights"], peel0, True, "HKY", 4)
+    post = Posterior(spec, tree, lik)
+    assert post.dim == 1 + (S - 2) + 1 + 1 + 1 + 1 + 3
+    case = cases.fluA_case()
+    vals = dict(wshape=0.488, rate=0.00499, height=d["heights"][-1], theta=4.03, kappa=5.58,
+                freqs=case.freqs, props=post.props_from_heights(d["heights"]))
+    u = post.unconstrain(vals)
+    np.testing.assert_allclose(post.blens(u[None])[0], case.blens, rtol=1e-12, atol=1e-15)
+    lp, g = check_grad(post, u, tol=5e-6)
+    names = post.column_names()
+    assert names[:3] == ["wshape", "props.1", "props.2"]
+    assert "heights.68" in names and names.index("ps.1") < names.index("rs.1") < names.index("heights.1")
+
+
+def test_batched_equals_single():
+    post, rng = _random_posterior(4, model="GTR", C=4, clock="strict", coalescent="constant")
+    U = rng.uniform(-1, 1, (3, post.dim))
+    lp, G = post.log_prob_grad(U)
+    for k in range(3):
+        l1, g1 = post.log_prob_grad(U[k:k + 1])
+        assert abs(l1[0] - lp[k]) <= 1e-13 * abs(lp[k])
+        np.testing.assert_allclose(g1[0], G[k], rtol=1e-13, atol=1e-12)
+
+
+def test_unsupported_options_are_loud():
+    with pytest.raises(NotImplementedError):
+        ModelSpec(model="GTR", clock="ucln")
+    with pytest.raises(ValueError):
+        ModelSpec(model="GTR", categories=4, invariant=True, heterogeneity="discrete")
