@@ -1,0 +1,221 @@
+"""Mean-field ADVI -- the optimiser behind ``phylostan run -a vb`` (the
+default; ``phylostan/phylostan.py:302-317``: ``sm.vb(tol_rel_obj,
+elbo_samples, grad_samples, iter, eta, algorithm='meanfield')``).
+
+Algorithm: Stan's ``advi<Model, normal_meanfield>``: the approximation
+N(mu, diag(exp(omega)^2)) starts at the initial point with omega = 0;
+``adapt_eta`` tries eta in (100, 10, 1, 0.1, 0.01) for ``adapt_iter`` (50)
+steps each; ``stochastic_gradient_ascent`` uses the adaGrad-like sequence
+(history 0.9 / 0.1, tau 1, eta / sqrt(iter)); every ``eval_elbo`` (100)
+iterations the ELBO is estimated with ``elbo_samples`` draws and the
+relative ELBO change goes into a circular buffer of
+max(0.1 max_iter / eval_elbo, 2) entries whose mean or median below
+``tol_rel_obj`` stops the run.  The ELBO uses ``log_prob<propto=false>``
+(constants included), the gradient ``log_prob<propto=true>``; the entropy
+is ``dim/2 (1 + log 2 pi) + sum omega``.
+
+MI355X shape: the ``elbo_samples`` draws of each ELBO estimate (default 100)
+are ONE batched likelihood launch, as are the ``grad_samples`` draws of each
+gradient.
+"""
+import math
+import time
+
+import numpy as np
+
+ETA_SEQUENCE = (100.0, 10.0, 1.0, 0.1, 0.01)
+
+
+class ADVIError(RuntimeError):
+    pass
+
+
+class MeanField:
+    def __init__(self, mu, omega=None):
+        self.mu = np.asarray(mu, np.float64).copy()
+        self.omega = np.zeros_like(self.mu) if omega is None else np.asarray(omega, np.float64).copy()
+
+    def copy(self):
+        return MeanField(self.mu, self.omega)
+
+    def entropy(self):
+        return 0.5 * len(self.mu) * (1.0 + math.log(2.0 * math.pi)) + float(self.omega.sum())
+
+    def transform(self, eta):
+        return self.mu + np.exp(self.omega) * eta
+
+    def sample(self, rng, n):
+        return self.transform(rng.standard_normal((n, len(self.mu))))
+
+
+class ADVI:
+    def __init__(self, posterior, rng, grad_samples=1, elbo_samples=100, eval_elbo=100, log=print):
+        self.post = posterior
+        self.rng = rng
+        self.grad_samples = int(grad_samples)
+        self.elbo_samples = int(elbo_samples)
+        self.eval_elbo = int(eval_elbo)
+        self.log = log or (lambda *_: None)
+        self.n_grad = 0
+        self.n_lp = 0
+
+    # ------------------------------------------------------------ estimates
+    def calc_elbo(self, q):
+        """Monte-Carlo ELBO; non-finite draws are dropped and redrawn (at most
+        elbo_samples of them), as calc_ELBO does."""
+        need = self.elbo_samples
+        got, total, dropped = 0, 0.0, 0
+        while got < self.elbo_samples:
+            Z = q.sample(self.rng, need)
+            lp = self.post.log_prob(Z, propto=False)
+            self.n_lp += len(Z)
+            ok = np.isfinite(lp)
+            total += float(lp[ok].sum())
+            got += int(ok.sum())
+            dropped += int((~ok).sum())
+            if dropped >= self.elbo_samples:
+                raise ADVIError("The number of dropped evaluations has reached its maximum amount (%d)."
+                                % self.elbo_samples)
+            need = self.elbo_samples - got
+        return total / self.elbo_samples + q.entropy()
+
+    def calc_elbo_grad(self, q):
+        dim = len(q.mu)
+        mu_g = np.zeros(dim)
+        om_g = np.zeros(dim)
+        got, drops = 0, 0
+        while got < self.grad_samples:
+            need = self.grad_samples - got
+            eta = self.rng.standard_normal((need, dim))
+            Z = q.transform(eta)
+            lp, G = self.post.log_prob_grad(Z)
+            self.n_grad += need
+            for k in range(need):
+                if np.isfinite(lp[k]) and np.all(np.isfinite(G[k])):
+                    mu_g += G[k]
+                    om_g += G[k] * eta[k]
+                    got += 1
+                else:
+                    drops += 1
+                    if drops >= 10 * self.grad_samples:
+                        raise ADVIError("stan::variational::normal_meanfield::calc_grad: The number of dropped "
+                                        "evaluations has reached its maximum amount (%d)." % (10 * self.grad_samples))
+        mu_g /= self.grad_samples
+        om_g /= self.grad_samples
+        om_g = om_g * np.exp(q.omega) + 1.0
+        return mu_g, om_g
+
+    @staticmethod
+    def _step(q, gm, go, hist_m, hist_o, it, eta, first):
+        if first:
+            hist_m += gm * gm
+            hist_o += go * go
+        else:
+            hist_m *= 0.9
+            hist_m += 0.1 * gm * gm
+            hist_o *= 0.9
+            hist_o += 0.1 * go * go
+        es = eta / math.sqrt(it)
+        q.mu += es * gm / (1.0 + np.sqrt(hist_m))
+        q.omega += es * go / (1.0 + np.sqrt(hist_o))
+
+    # ------------------------------------------------------------ phases
+    def adapt_eta(self, q0, adapt_iter=50):
+        try:
+            elbo_init = self.calc_elbo(q0)
+        except ADVIError:
+            raise ADVIError("Cannot compute ELBO using the initial variational distribution.")
+        self.log("Begin eta adaptation.")
+        elbo_best, eta_best = -math.inf, 0.0
+        dim = len(q0.mu)
+        for k, eta in enumerate(ETA_SEQUENCE):
+            q = q0.copy()
+            hm, ho = np.zeros(dim), np.zeros(dim)
+            for it in range(1, adapt_iter + 1):
+                try:
+                    gm, go = self.calc_elbo_grad(q)
+                except ADVIError:
+                    gm, go = np.zeros(dim), np.zeros(dim)
+                self._step(q, gm, go, hm, ho, it, eta, it == 1)
+                m = k * adapt_iter + it
+                if m == 1 or m % adapt_iter == 0:
+                    self.log("Iteration: %3d / %d [%3d%%]  (Adaptation)"
+                             % (m, adapt_iter * len(ETA_SEQUENCE), 100 * m // (adapt_iter * len(ETA_SEQUENCE))))
+            try:
+                elbo = self.calc_elbo(q)
+            except ADVIError:
+                elbo = -math.inf
+            if not np.isfinite(elbo):
+                elbo = -math.inf
+            if elbo < elbo_best and elbo_best > elbo_init:
+                self.log("Success! Found best value [eta = %g]%s" % (eta_best, " earlier than expected."
+                                                                   if k < len(ETA_SEQUENCE) - 1 else "."))
+                self.log("")
+                return eta_best
+            if k < len(ETA_SEQUENCE) - 1:
+                elbo_best, eta_best = elbo, eta
+            else:
+                if elbo > elbo_init:
+                    self.log("Success! Found best value [eta = %g]." % eta_best)
+                    self.log("")
+                    return eta
+                raise ADVIError("All proposed step-sizes failed. Your model may be either severely "
+                                "ill-conditioned or misspecified.")
+        return eta_best
+
+    def sga(self, q, eta, tol_rel_obj, max_iterations, diag=None):
+        """stochastic_gradient_ascent; ``diag(iter, seconds, elbo)`` per ELBO
+        evaluation (the rows of the .diag file)."""
+        dim = len(q.mu)
+        hm, ho = np.zeros(dim), np.zeros(dim)
+        cb_size = int(max(0.1 * max_iterations / self.eval_elbo, 2.0))
+        cb = []
+        elbo, elbo_best = 0.0, -math.inf
+        self.log("Begin stochastic gradient ascent.")
+        self.log("  iter             ELBO   delta_ELBO_mean   delta_ELBO_med   notes ")
+        t0 = time.time()
+        it = 0
+        while True:
+            it += 1
+            gm, go = self.calc_elbo_grad(q)
+            self._step(q, gm, go, hm, ho, it, eta, it == 1)
+            done = False
+            if it % self.eval_elbo == 0:
+                elbo_prev = elbo
+                elbo = self.calc_elbo(q)
+                elbo_best = max(elbo_best, elbo)
+                delta = abs((elbo_prev - elbo) / elbo)
+                cb.append(delta)
+                if len(cb) > cb_size:
+                    cb.pop(0)
+                ave = float(np.mean(cb))
+                med = float(np.median(cb))
+                line = "  %4d  %15.3f  %16.3f  %15.3f" % (it, elbo, ave, med)
+                if diag:
+                    diag(it, time.time() - t0, elbo)
+                if ave < tol_rel_obj:
+                    line += "   MEAN ELBO CONVERGED"
+                    done = True
+                if med < tol_rel_obj:
+                    line += "   MEDIAN ELBO CONVERGED"
+                    done = True
+                if it > 10 * self.eval_elbo and (med > 0.5 or ave > 0.5):
+                    line += "   MAY BE DIVERGING... INSPECT ELBO"
+                self.log(line)
+                if done and abs((elbo_best - elbo) / elbo) > 0.05:
+                    self.log("Informational Message: The ELBO at a previous iteration is larger than the ELBO "
+                             "upon convergence!")
+            if it == max_iterations:
+                self.log("Informational Message: The maximum number of iterations is reached! The algorithm "
+                         "may not have converged.")
+                done = True
+            if done:
+                return q, it
+
+    def run(self, q0_mu, eta=None, adapt_engaged=True, adapt_iter=50, tol_rel_obj=0.01,
+            max_iterations=10000, diag=None):
+        q0 = MeanField(q0_mu)
+        if adapt_engaged or eta is None:
+            eta = self.adapt_eta(q0, adapt_iter)
+        q, iters = self.sga(q0.copy(), eta, tol_rel_obj, max_iterations, diag)
+        return q, eta, iters

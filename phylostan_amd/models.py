@@ -116,8 +116,8 @@ def q_param_gradients(dLdP, blens, rs, freqs, rates, grad_freq_root=None):
     """
     Q, lam, V, Vinv, R, Qt, s = eigen_system(freqs, rates)
     t = np.asarray(rs)[:, None] * np.asarray(blens)[None, :]  # [C, B]
-    H = np.einsum("jk,cbjl,ml->cbkm", V, dLdP, Vinv)  # V^T G V^-T
-    M = np.einsum("cbkl,cbkl->kl", H, _phi(lam, t))
+    H = np.matmul(np.matmul(V.T, dLdP), Vinv.T)  # V^T G V^-T per (c, b)
+    M = (H * _phi(lam, t)).sum(axis=(0, 1))
     f = np.asarray(freqs, np.float64)
 
     def contract(dQt, ds):

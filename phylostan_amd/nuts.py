@@ -1,0 +1,328 @@
+"""Adaptive NUTS with a diagonal metric -- the sampler behind
+``phylostan run -a nuts`` (``phylostan/phylostan.py:318-321``:
+``sm.sampling(algorithm='NUTS', chains, iter, thin, seed)``).
+
+Algorithm: Stan's ``adapt_diag_e_nuts`` (multinomial trajectory sampling
+with the across-subtree no-U-turn checks of ``base_nuts::transition`` /
+``build_tree``; leapfrog ``expl_leapfrog``; Nesterov dual-averaging step
+size, delta 0.8, gamma 0.05, kappa 0.75, t0 10; windowed variance
+adaptation, init buffer 75, term buffer 50, base window 25, regularised
+``n/(n+5) var + 1e-3 * 5/(n+5)``; ``init_stepsize`` doubling/halving;
+max tree depth 10; max Delta-H 1000).  Stan's boost RNG streams are not
+reproduced (numpy PCG64 per chain).
+
+MI355X shape: every chain is a *coroutine* that yields the positions whose
+log density and gradient it needs; ``run_chains`` advances all chains in
+lockstep and evaluates the pending positions of all of them in ONE batched
+call (one GPU launch of ``n_chains`` draws), so 8 chains cost about as much
+wall time per leapfrog step as one.
+"""
+import math
+import time
+
+import numpy as np
+
+
+def _log_sum_exp(a, b):
+    if a == -math.inf:
+        return b
+    if b == -math.inf:
+        return a
+    m = max(a, b)
+    return m + math.log(math.exp(a - m) + math.exp(b - m))
+
+
+class _Point:
+    __slots__ = ("q", "p", "lp", "g")
+
+    def __init__(self, q, p, lp, g):
+        self.q, self.p, self.lp, self.g = q, p, lp, g
+
+    def copy(self):
+        return _Point(self.q.copy(), self.p.copy(), self.lp, self.g.copy())
+
+
+class Chain:
+    """One NUTS chain as a generator (``program()``): it yields a position
+    ``q`` and expects ``(lp, grad)`` sent back; it records its draws."""
+
+    def __init__(self, dim, q0, rng, num_warmup=1000, num_samples=1000, thin=1, max_depth=10,
+                 delta=0.8, gamma=0.05, kappa=0.75, t0=10.0, stepsize=1.0, init_buffer=75,
+                 term_buffer=50, base_window=25, max_delta_h=1000.0):
+        self.dim = dim
+        self.q0 = np.asarray(q0, np.float64).copy()
+        self.rng = rng
+        self.num_warmup = int(num_warmup)
+        self.num_samples = int(num_samples)
+        self.thin = max(1, int(thin))
+        self.max_depth = max_depth
+        self.delta, self.gamma, self.kappa, self.t0 = delta, gamma, kappa, t0
+        self.eps = float(stepsize)
+        self.max_delta_h = max_delta_h
+        self.inv_metric = np.ones(dim)
+        self._setup_windows(init_buffer, term_buffer, base_window)
+        self.draws = []  # (q, lp, accept, eps, depth, n_leapfrog, divergent, energy, warmup)
+        self.n_grad = 0
+
+    # -------------------------------------------------------- adaptation
+    def _setup_windows(self, init_buffer, term_buffer, base_window):
+        W = self.num_warmup
+        if W < 20:
+            self.adapt_init, self.adapt_term, self.adapt_base = W, 0, 0
+            self.windows = False
+            return
+        self.windows = True
+        if init_buffer + base_window + term_buffer > W:
+            init_buffer = int(0.15 * W)
+            term_buffer = int(0.1 * W)
+            base_window = W - (init_buffer + term_buffer)
+        self.adapt_init, self.adapt_term, self.adapt_base = init_buffer, term_buffer, base_window
+        self.win_counter = 0
+        self.win_size = base_window
+        self.next_window = init_buffer + base_window - 1
+        self._w_n = 0
+        self._w_mean = np.zeros(self.dim)
+        self._w_m2 = np.zeros(self.dim)
+
+    def _in_window(self):
+        W = self.num_warmup
+        return self.adapt_init <= self.win_counter < W - self.adapt_term and self.win_counter != W
+
+    def _end_window(self):
+        return self.win_counter == self.next_window and self.win_counter != self.num_warmup
+
+    def _compute_next_window(self):
+        W, term = self.num_warmup, self.adapt_term
+        if self.next_window == W - term - 1:
+            return
+        self.win_size *= 2
+        self.next_window = self.win_counter + self.win_size
+        if self.next_window != W - term - 1:
+            if self.next_window + 2 * self.win_size >= W - term:
+                self.next_window = W - term - 1
+
+    def _learn_variance(self, q):
+        if not self.windows:
+            return False
+        if self._in_window():
+            self._w_n += 1
+            d = q - self._w_mean
+            self._w_mean += d / self._w_n
+            self._w_m2 += d * (q - self._w_mean)
+        if self._end_window():
+            self._compute_next_window()
+            n = float(self._w_n)
+            var = self._w_m2 / (n - 1.0) if n > 1 else np.ones(self.dim)
+            self.inv_metric = (n / (n + 5.0)) * var + 1e-3 * (5.0 / (n + 5.0))
+            self._w_n = 0
+            self._w_mean[:] = 0.0
+            self._w_m2[:] = 0.0
+            self.win_counter += 1
+            return True
+        self.win_counter += 1
+        return False
+
+    def _da_restart(self):
+        self.da_counter = 0
+        self.s_bar = 0.0
+        self.x_bar = 0.0
+        self.mu = math.log(10.0 * self.eps)
+
+    def _learn_stepsize(self, adapt_stat):
+        self.da_counter += 1
+        adapt_stat = min(1.0, adapt_stat)
+        eta = 1.0 / (self.da_counter + self.t0)
+        self.s_bar = (1.0 - eta) * self.s_bar + eta * (self.delta - adapt_stat)
+        x = self.mu - self.s_bar * math.sqrt(self.da_counter) / self.gamma
+        x_eta = self.da_counter ** (-self.kappa)
+        self.x_bar = (1.0 - x_eta) * self.x_bar + x_eta * x
+        self.eps = math.exp(x)
+
+    # ------------------------------------------------------ hamiltonian
+    def _sample_p(self):
+        return self.rng.standard_normal(self.dim) / np.sqrt(self.inv_metric)
+
+    def _H(self, z):
+        if not np.isfinite(z.lp):
+            return math.inf
+        return -z.lp + 0.5 * float(np.dot(self.inv_metric * z.p, z.p))
+
+    def _evolve(self, z, eps):
+        """expl_leapfrog: one step in place; yields the new q for (lp, grad)."""
+        z.p = z.p + 0.5 * eps * z.g
+        z.q = z.q + eps * self.inv_metric * z.p
+        lp, g = yield z.q
+        self.n_grad += 1
+        z.lp = lp
+        z.g = g if np.all(np.isfinite(g)) else np.zeros_like(z.q)
+        if not np.isfinite(lp):
+            z.lp = -math.inf
+        z.p = z.p + 0.5 * eps * z.g
+
+    def _init_stepsize(self, z0):
+        if self.eps == 0 or self.eps > 1e7 or math.isnan(self.eps):
+            return
+        z = z0.copy()
+        z.p = self._sample_p()
+        H0 = self._H(z)
+        yield from self._evolve(z, self.eps)
+        h = self._H(z)
+        dH = H0 - (math.inf if math.isnan(h) else h)
+        direction = 1 if dH > math.log(0.8) else -1
+        while True:
+            z = z0.copy()
+            z.p = self._sample_p()
+            H0 = self._H(z)
+            yield from self._evolve(z, self.eps)
+            h = self._H(z)
+            dH = H0 - (math.inf if math.isnan(h) else h)
+            if direction == 1 and not dH > math.log(0.8):
+                break
+            if direction == -1 and not dH < math.log(0.8):
+                break
+            self.eps = self.eps * 2.0 if direction == 1 else self.eps * 0.5
+            if self.eps > 1e7:
+                raise RuntimeError("NUTS: posterior is improper (step size > 1e7)")
+            if self.eps == 0:
+                raise RuntimeError("NUTS: no acceptable small step size")
+
+    @staticmethod
+    def _criterion(ps_minus, ps_plus, rho):
+        return float(np.dot(ps_plus, rho)) > 0 and float(np.dot(ps_minus, rho)) > 0
+
+    def _build_tree(self, depth, z, H0, sign, st):
+        """Returns (valid, z_propose, p_sharp_beg, p_sharp_end, rho, p_beg,
+        p_end, log_sum_weight); ``st`` carries n_leapfrog, sum_metro_prob,
+        divergent.  ``z`` is advanced in place."""
+        if depth == 0:
+            yield from self._evolve(z, sign * self.eps)
+            st["n_leapfrog"] += 1
+            h = self._H(z)
+            if math.isnan(h):
+                h = math.inf
+            if h - H0 > self.max_delta_h:
+                st["divergent"] = True
+            lsw = H0 - h if h != math.inf else -math.inf
+            st["sum_metro_prob"] += 1.0 if H0 - h > 0 else math.exp(H0 - h)
+            ps = self.inv_metric * z.p
+            return (not st["divergent"], z.copy(), ps, ps.copy(), z.p.copy(), z.p.copy(), z.p.copy(), lsw)
+        v1, zp, ps_beg, ps_init_end, rho_init, p_beg, p_init_end, lsw_init = \
+            yield from self._build_tree(depth - 1, z, H0, sign, st)
+        if not v1:
+            return (False, zp, ps_beg, ps_init_end, rho_init, p_beg, p_init_end, lsw_init)
+        v2, zp_final, ps_final_beg, ps_end, rho_final, p_final_beg, p_end, lsw_final = \
+            yield from self._build_tree(depth - 1, z, H0, sign, st)
+        if not v2:
+            return (False, zp, ps_beg, ps_end, rho_init, p_beg, p_end, lsw_init)
+        lsw_sub = _log_sum_exp(lsw_init, lsw_final)
+        if lsw_final > lsw_sub:
+            zp = zp_final
+        else:
+            if self.rng.uniform() < math.exp(lsw_final - lsw_sub):
+                zp = zp_final
+        rho_sub = rho_init + rho_final
+        ok = self._criterion(ps_beg, ps_end, rho_sub)
+        ok &= self._criterion(ps_beg, ps_final_beg, rho_init + p_final_beg)
+        ok &= self._criterion(ps_init_end, ps_end, rho_final + p_init_end)
+        return (ok, zp, ps_beg, ps_end, rho_sub, p_beg, p_end, lsw_sub)
+
+    def _transition(self, z0):
+        z = z0.copy()
+        z.p = self._sample_p()
+        H0 = self._H(z)
+        z_fwd, z_bck, z_sample = z.copy(), z.copy(), z.copy()
+        ps0 = self.inv_metric * z.p
+        p_fwd_fwd = z.p.copy(); ps_fwd_fwd = ps0.copy()
+        p_fwd_bck = z.p.copy(); ps_fwd_bck = ps0.copy()
+        p_bck_fwd = z.p.copy(); ps_bck_fwd = ps0.copy()
+        p_bck_bck = z.p.copy(); ps_bck_bck = ps0.copy()
+        rho = z.p.copy()
+        lsw = 0.0
+        st = {"n_leapfrog": 0, "sum_metro_prob": 0.0, "divergent": False}
+        depth = 0
+        while depth < self.max_depth:
+            if self.rng.uniform() > 0.5:
+                rho_bck = rho
+                p_bck_fwd, ps_bck_fwd = p_fwd_bck, ps_fwd_bck
+                zz = z_fwd
+                valid, zp, ps_fwd_bck, ps_fwd_fwd, rho_fwd, p_fwd_bck, p_fwd_fwd, lsw_sub = \
+                    yield from self._build_tree(depth, zz, H0, 1.0, st)
+                z_fwd = zz
+            else:
+                rho_fwd = rho
+                p_fwd_bck, ps_fwd_bck = p_bck_fwd, ps_bck_fwd
+                zz = z_bck
+                valid, zp, ps_bck_fwd, ps_bck_bck, rho_bck, p_bck_fwd, p_bck_bck, lsw_sub = \
+                    yield from self._build_tree(depth, zz, H0, -1.0, st)
+                z_bck = zz
+            if not valid:
+                break
+            depth += 1
+            if lsw_sub > lsw:
+                z_sample = zp
+            elif self.rng.uniform() < math.exp(lsw_sub - lsw):
+                z_sample = zp
+            lsw = _log_sum_exp(lsw, lsw_sub)
+            rho = rho_bck + rho_fwd
+            ok = self._criterion(ps_bck_bck, ps_fwd_fwd, rho)
+            ok &= self._criterion(ps_bck_bck, ps_fwd_bck, rho_bck + p_fwd_bck)
+            ok &= self._criterion(ps_bck_fwd, ps_fwd_fwd, rho_fwd + p_bck_fwd)
+            if not ok:
+                break
+        n_lf = st["n_leapfrog"]
+        accept = st["sum_metro_prob"] / max(n_lf, 1)
+        energy = self._H(z_sample)
+        return z_sample, accept, depth, n_lf, st["divergent"], energy
+
+    # ----------------------------------------------------------- program
+    def program(self):
+        lp, g = yield self.q0
+        z = _Point(self.q0.copy(), np.zeros(self.dim), lp, g)
+        if not np.isfinite(lp):
+            raise RuntimeError("NUTS: initial point has non-finite log density")
+        yield from self._init_stepsize(z)
+        self._da_restart()
+        total = self.num_warmup + self.num_samples
+        for it in range(total):
+            warm = it < self.num_warmup
+            eps_used = self.eps
+            z_new, accept, depth, n_lf, div, energy = yield from self._transition(z)
+            z = _Point(z_new.q, np.zeros(self.dim), z_new.lp, z_new.g)
+            if warm:
+                self._learn_stepsize(accept)
+                if self._learn_variance(z.q):
+                    yield from self._init_stepsize(z)
+                    self._da_restart()
+                if it == self.num_warmup - 1:
+                    self.eps = math.exp(self.x_bar)  # complete_adaptation
+            if it % self.thin == 0:
+                self.draws.append((z.q.copy(), z.lp, accept, eps_used, depth, n_lf, int(div), energy, warm))
+        return self
+
+
+def run_chains(posterior, q0s, seeds, num_warmup=1000, num_samples=1000, thin=1, progress=None,
+               max_depth=10, **kw):
+    """Run ``len(q0s)`` NUTS chains in lockstep, batching every round of
+    gradient requests into one ``posterior.log_prob_grad`` call."""
+    chains = [Chain(posterior.dim, q0, np.random.default_rng(sd), num_warmup, num_samples, thin,
+                    max_depth=max_depth, **kw) for q0, sd in zip(q0s, seeds)]
+    gens = [c.program() for c in chains]
+    pending = {}
+    for i, g in enumerate(gens):
+        pending[i] = next(g)
+    rounds = 0
+    t0 = time.time()
+    while pending:
+        idx = sorted(pending)
+        Q = np.stack([pending[i] for i in idx])
+        lp, G = posterior.log_prob_grad(Q)
+        for k, i in enumerate(idx):
+            try:
+                pending[i] = gens[i].send((float(lp[k]), G[k]))
+            except StopIteration:
+                del pending[i]
+        rounds += 1
+        if progress and rounds % 2000 == 0:
+            progress("NUTS: %d batched gradient rounds, %d draws (chain 0), %.1f s"
+                     % (rounds, len(chains[0].draws), time.time() - t0))
+    return chains

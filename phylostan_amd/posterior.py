@@ -379,10 +379,19 @@ class Posterior:
         else:
             blens = vals["blens"]
 
-        # ---- likelihood (GPU)
+        # ---- likelihood (GPU); draws whose parameters over/underflowed in the
+        # transforms are rejected without a launch (Stan: domain error)
         mv = np.concatenate([freqs, R, rs, ps], axis=1)
-        res = self.lik.evaluate_batch(blens, mv)
-        ll = np.array([r.loglik for r in res])
+        ok = (np.isfinite(lp) & np.all(np.isfinite(mv), axis=1) & np.all(np.isfinite(blens), axis=1)
+              & np.all(freqs > 0, axis=1))
+        ll = np.full(n, -np.inf)
+        res = [None] * n
+        if ok.any():
+            sel = np.nonzero(ok)[0]
+            out = self.lik.evaluate_batch(blens[sel], mv[sel])
+            for k, r in zip(sel, out):
+                res[k] = r
+                ll[k] = r.loglik
         lp = lp + ll
         bad = ~np.isfinite(lp)
 
@@ -439,11 +448,14 @@ class Posterior:
             return lp, None
 
         # ---- likelihood gradient -> constrained parameters
-        g_bl = np.stack([r.grad_blens for r in res])
-        g_rs = np.stack([r.grad_rs for r in res])
-        g_ps = np.stack([r.grad_ps for r in res])
+        zb, zc = np.zeros(self.B), np.zeros(C)
+        g_bl = np.stack([r.grad_blens if r is not None else zb for r in res])
+        g_rs = np.stack([r.grad_rs if r is not None else zc for r in res])
+        g_ps = np.stack([r.grad_ps if r is not None else zc for r in res])
         if sp.model != "JC69":
             for d in range(n):
+                if bad[d]:
+                    continue
                 gr, gf = models.q_param_gradients(res[d].dLdP, blens[d], rs[d], freqs[d], R[d],
                                                   res[d].grad_freq_root)
                 gx["freqs"][d] += gf
@@ -475,6 +487,7 @@ class Posterior:
         for p in self.params:
             G[:, p.sl] = p.tr.backward(states[p.name], gx[p.name], 1.0)
         G[bad] = 0.0
+        G[~np.isfinite(G)] = 0.0
         return lp, G
 
     def _site_rates_backward(self, vals, g_rs, g_ps, gx, rs, ps):

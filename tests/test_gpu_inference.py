@@ -1,0 +1,78 @@
+"""GPU: the posterior, ADVI and NUTS driven by the HIP likelihood (C-ABI).
+
+* the host posterior around ``TreeLikelihood`` equals the one around the
+  CPU oracle (value rel 1e-10, gradient 1e-8 of its largest entry);
+* ``phylostan run -a vb`` on fluA (HKY+W4, strict clock, constant
+  coalescent, heterochronous -- the README.md:93-109 analysis) lands its
+  posterior means inside the 95% credible intervals the reference prints
+  there;
+* a short multi-chain NUTS run on fluA is finite and moves uphill.
+"""
+import numpy as np
+import pytest
+
+from tests import cases, fixture_files
+from tests.oracle_backend import OracleLikelihood
+
+pytestmark = pytest.mark.gpu
+
+README_CI = {  # README.md:104-108 (fluA meanfield ADVI)
+    "wshape": (0.383, 0.616),
+    "rate": (0.00432, 0.00577),
+    "theta": (3.14, 5.05),
+    "kappa": (4.37, 7.039),
+    "root_height": (18.36, 19.74),
+}
+
+
+def _fluA_posterior(lik_cls, **kw):
+    from phylostan_amd.posterior import ModelSpec, Posterior, TreeData
+    d = cases.load_layout("fluA")
+    S = d["tipbits"].shape[0]
+    peel0 = d["peel"] - 1
+    tree = TreeData(S, peel0, d["map"], d["lowers"], float(d["oldest"]))
+    spec = ModelSpec(model="HKY", categories=4, clock="strict", estimate_rate=True, coalescent="constant",
+                     heterochronous=True)
+    return Posterior(spec, tree, lik_cls(d["tipbits"], d["weights"], peel0, True, "HKY", 4, **kw)), d
+
+
+def test_posterior_gpu_equals_oracle():
+    from phylostan_amd.engine import TreeLikelihood
+    pg, d = _fluA_posterior(TreeLikelihood, max_draws=8)
+    po, _ = _fluA_posterior(OracleLikelihood)
+    case = cases.fluA_case()
+    u0 = pg.unconstrain(dict(wshape=0.488, rate=0.00499, height=d["heights"][-1], theta=4.03, kappa=5.58,
+                             freqs=case.freqs, props=pg.props_from_heights(d["heights"])))
+    rng = np.random.default_rng(0)
+    U = np.stack([u0] + [u0 + 0.05 * rng.standard_normal(pg.dim) for _ in range(3)])
+    lg, Gg = pg.log_prob_grad(U)
+    lo, Go = po.log_prob_grad(U)
+    np.testing.assert_allclose(lg, lo, rtol=1e-10)
+    for k in range(len(U)):
+        assert np.max(np.abs(Gg[k] - Go[k])) <= 1e-8 * np.max(np.abs(Go[k]))
+
+
+def test_fluA_advi_within_readme_intervals(tmp_path):
+    from phylostan_amd import cli, stan_io
+    t, a = fixture_files.write_dataset("fluA", str(tmp_path))
+    out = str(tmp_path / "fluA")
+    cli.main(["run", "-s", str(tmp_path / "fluA.json"), "-m", "HKY", "-C", "4", "--heterochronous",
+              "--estimate_rate", "--clock", "strict", "--coalescent", "constant", "-i", a, "-t", t, "-o", out,
+              "-q", "meanfield", "-S", "1", "--iter", "30000"])
+    res = stan_io.parse_log(out, 0.05)
+    for key, (lo, hi) in README_CI.items():
+        m = res[key][0]
+        assert lo <= m <= hi, "%s mean %g outside the reference's 95%% CI (%g, %g)" % (key, m, lo, hi)
+
+
+def test_fluA_nuts_short_multichain():
+    from phylostan_amd.engine import TreeLikelihood
+    from phylostan_amd.nuts import run_chains
+    post, d = _fluA_posterior(TreeLikelihood, max_draws=4)
+    rng = np.random.default_rng(5)
+    q0s = [post.initial_point(rng) for _ in range(4)]
+    lp0 = post.log_prob(np.stack(q0s))
+    chains = run_chains(post, q0s, [11, 12, 13, 14], num_warmup=40, num_samples=10, max_depth=6)
+    for c, ch in enumerate(chains):
+        lps = np.array([dr[1] for dr in ch.draws])
+        assert np.all(np.isfinite(lps)) and lps[-1] > lp0[c]

@@ -1,0 +1,92 @@
+"""NUTS and mean-field ADVI (phylostan_amd/nuts.py, advi.py) on targets with
+known answers, and the batched multi-chain driver."""
+import math
+
+import numpy as np
+import pytest
+
+from phylostan_amd import nuts
+from phylostan_amd.advi import ADVI
+
+
+class Gauss:
+    """Independent normal target N(mu, sd^2) with a batched log_prob_grad."""
+
+    def __init__(self, mu, sd):
+        self.mu = np.asarray(mu, np.float64)
+        self.sd = np.asarray(sd, np.float64)
+        self.dim = len(self.mu)
+        self.batches = []
+
+    def log_prob_grad(self, Q, propto=True, need_grad=True):
+        Q = np.atleast_2d(Q)
+        self.batches.append(len(Q))
+        z = (Q - self.mu) / self.sd
+        lp = -0.5 * (z * z).sum(1)
+        if not propto:
+            lp = lp - np.log(self.sd).sum() - 0.5 * self.dim * math.log(2 * math.pi)
+        return lp, (-(Q - self.mu) / self.sd ** 2 if need_grad else None)
+
+    def log_prob(self, Q, propto=True):
+        return self.log_prob_grad(Q, propto, False)[0]
+
+
+def test_nuts_recovers_gaussian_moments():
+    mu = np.array([1.0, -2.0, 0.5, 3.0])
+    sd = np.array([0.1, 1.0, 5.0, 0.01])
+    tgt = Gauss(mu, sd)
+    chains = nuts.run_chains(tgt, [np.zeros(4)], [1], num_warmup=500, num_samples=2000)
+    ch = chains[0]
+    X = np.stack([d[0] for d in ch.draws if not d[8]])
+    assert X.shape == (2000, 4)
+    se = sd / math.sqrt(2000) * 4  # generous: autocorrelation
+    assert np.all(np.abs(X.mean(0) - mu) < 5 * se)
+    np.testing.assert_allclose(X.std(0), sd, rtol=0.15)
+    # adapted metric ~ posterior variance, acceptance near delta
+    np.testing.assert_allclose(ch.inv_metric, sd ** 2, rtol=0.5)
+    acc = np.mean([d[2] for d in ch.draws if not d[8]])
+    assert 0.6 < acc < 0.98
+    assert all(d[6] == 0 for d in ch.draws if not d[8])
+
+
+def test_nuts_chains_are_batched():
+    tgt = Gauss(np.zeros(3), np.ones(3))
+    chains = nuts.run_chains(tgt, [np.full(3, 0.5 * k) for k in range(4)], [10 + k for k in range(4)],
+                             num_warmup=50, num_samples=50)
+    assert len(chains) == 4 and all(len(c.draws) == 100 for c in chains)
+    assert max(tgt.batches) == 4  # one evaluation call serves every pending chain
+
+
+def test_nuts_window_schedule_matches_stan():
+    ch = nuts.Chain(2, np.zeros(2), np.random.default_rng(0), num_warmup=1000)
+    ends = []
+    for it in range(1000):
+        if ch._end_window():
+            ends.append(it)
+            ch._compute_next_window()
+        ch.win_counter += 1
+    # Stan: windows 25, 50, 100, 200, 500 after a 75-iteration init buffer, last ends at 949
+    assert ends == [99, 149, 249, 449, 949]
+
+
+def test_advi_meanfield_gaussian():
+    mu = np.array([2.0, -1.0, 0.3])
+    sd = np.array([0.5, 2.0, 0.05])
+    tgt = Gauss(mu, sd)
+    adv = ADVI(tgt, np.random.default_rng(3), grad_samples=1, elbo_samples=100, log=None)
+    q, eta, iters = adv.run(np.zeros(3), tol_rel_obj=0.001, max_iterations=20000)
+    np.testing.assert_allclose(q.mu, mu, atol=3 * sd.max() * 0.2)
+    np.testing.assert_allclose(np.exp(q.omega), sd, rtol=0.3)
+    # exact ELBO of the optimum for a Gaussian target = 0 (propto=False, KL=0)
+    assert abs(adv.calc_elbo(q)) < 0.5
+    assert max(tgt.batches) == 100  # the 100 ELBO draws are one batched call
+
+
+def test_advi_all_eta_fail_is_loud():
+    class Bad(Gauss):
+        def log_prob_grad(self, Q, propto=True, need_grad=True):
+            Q = np.atleast_2d(Q)
+            return np.full(len(Q), -np.inf), np.zeros_like(Q)
+
+    with pytest.raises(RuntimeError):
+        ADVI(Bad(np.zeros(2), np.ones(2)), np.random.default_rng(0), log=None).run(np.zeros(2))
