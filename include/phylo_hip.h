@@ -94,8 +94,9 @@ const char* phy_last_error(void);
 
 int phy_num_branches(const phy_ctx* ctx);
 int phy_output_len(const phy_ctx* ctx);
-/* Traversal-program facts: steps (= S-1), partial slots, LDS stack depth,
- * pattern blocks of 64. */
+/* Traversal-program facts: steps (= S-1), partial slots, deep-stack entries
+ * (operands that wait while a sibling subtree runs), pattern blocks of the
+ * current column plan. */
 int phy_program_info(const phy_ctx* ctx, int* nsteps, int* nslots, int* depth, int* nblocks);
 
 /* Log-likelihood + full gradient of n_draws parameter points, host buffers,
@@ -127,14 +128,13 @@ int phy_timing_start(phy_ctx* ctx);
 int phy_timing_read(phy_ctx* ctx, double* total_ms, int* launches);
 
 /* Tuning: persistent workgroup budget per launch (0 = keep), columns per
- * lane `cols` (0 = automatic, 1 or 2) and the LDS bytes one workgroup may
- * use (0 = keep; smaller budgets stage the P-matrices and dL/dP
- * accumulators in more chunks).  The automatic plan (no PHY_LDS_BUDGET, no
- * PHY_COLS, nothing set here) takes the first of: two columns at 80 KiB
- * (two workgroups per CU), two columns at 160 KiB, one column at 80 KiB
- * that keeps LDS chunks of >= 24 matrices.  The environment variables
- * PHY_WG_BUDGET, PHY_COLS and PHY_LDS_BUDGET set the defaults at
- * phy_create. */
+ * lane `cols` (0 = automatic: 2 for C <= 8, else 1) and the LDS bytes one
+ * workgroup may use (0 = keep; smaller budgets stage the P-matrix records
+ * in more chunks).  The automatic LDS plan (no PHY_LDS_BUDGET, nothing set
+ * here) takes the most workgroups per CU the kernel's register budget
+ * allows whose LDS share still holds chunks of >= 24 matrices (or the whole
+ * program).  The environment variables PHY_WG_BUDGET, PHY_COLS and
+ * PHY_LDS_BUDGET set the defaults at phy_create. */
 int phy_set_tuning(phy_ctx* ctx, int wg_budget, int cols, int lds_budget);
 
 /* The LDS plan the next launch will use: chunks per pass, matrices per
@@ -143,12 +143,6 @@ int phy_lds_plan(const phy_ctx* ctx, int* n_chunks, int* matrices_per_chunk, int
 
 /* Pattern columns each lane carries in the current plan (1 or 2). */
 int phy_columns_per_lane(const phy_ctx* ctx);
-
-/* Diagnostic builds only (-DPHY_STAMP=1): per-wave s_memtime stamps of the
- * last launch, [wg][C][8] = start, forward, root, reverse, end of first
- * block, end, realtime start, realtime end.  Returns values copied (0 in
- * normal builds). */
-int phy_debug_stamps(phy_ctx* ctx, unsigned long long* out, int n);
 
 #ifdef __cplusplus
 }

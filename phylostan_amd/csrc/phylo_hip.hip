@@ -53,14 +53,33 @@ namespace {
 
 constexpr int WAVE = 64;
 #ifndef PHY_ABLATE
-#define PHY_ABLATE 0  // diagnostic builds only: 1 no dL/dP accumulation, 2 no reverse pass, 4 no scratch stores
+#define PHY_ABLATE 0  // diagnostic builds only: 2 = no reverse pass
 #endif
-// Program step (8 ints): x, y (child codes: tip index >= 0, or -(slot+1) of
-// an internal child's stored moved partial), mx, my (matrix of a tip child,
-// -1 if internal), mv (matrix of the step's own branch, -1 at the root),
-// vslot (scratch slot of a_v, -1 at the root), flags (bit 0: mv is a real
-// branch, not the merged identity), node id.
-constexpr int STEP_INTS = 8;
+#ifndef PHY_FWD_COND
+#define PHY_FWD_COND 0
+#endif
+// Program step (STEP_INTS ints, host-built by build_program).
+constexpr int STEP_INTS = 16;
+enum {
+  ST_X = 0,  // child x: tip index >= 0, or -1 (internal)
+  ST_Y,      // child y: same
+  ST_MX,     // matrix of a tip x (its branch), -1 otherwise
+  ST_MY,     // matrix of a tip y
+  ST_MV,     // matrix of the step's own branch (-1: root / merged branch)
+  ST_VSLOT,  // scratch slot of a_v (-1 at the root)
+  ST_FLAGS,  // F_* below
+  ST_XSLOT,  // scratch slot of an internal x
+  ST_YSLOT,  // scratch slot of an internal y
+  ST_XDPOS,  // deep-stack entry of x when both children are internal
+  ST_VDPOS,  // deep-stack entry of v when F_VDEEP
+  ST_CHUNK,  // LDS chunk holding the step's matrices
+  ST_M0,     // first matrix of that chunk
+  ST_MN,     // matrices in that chunk
+  ST_NODE,   // node id
+};
+constexpr int F_MV = 1;     // the step's branch has a matrix (else identity)
+constexpr int F_XDEEP = 2;  // both children internal: x's operand is on the deep stack
+constexpr int F_VDEEP = 4;  // v is the x child of a both-internal parent
 // Per-draw eigensystem record: P(t) = m1 diag(exp(lam t)) m2, plus Q.
 constexpr int EIG_LEN = 56;  // m1[16] lam[4] m2[16] Q[16] (+pad)
 constexpr int EIG_M1 = 0, EIG_LAM = 16, EIG_M2 = 20, EIG_Q = 36;
@@ -82,8 +101,22 @@ int fail(int code, const std::string& msg) {
 // ---------------------------------------------------------------------------
 // device helpers
 // ---------------------------------------------------------------------------
+// Field-wise copies: an aggregate copy becomes a 32-B memcpy, and memcpys
+// on both sides of a branch get merged into one from a phi of the source
+// addresses, which pins the arrays in scratch.  Copying fields keeps every
+// V4 in registers.
 struct V4 {
   double x, y, z, w;
+  __host__ __device__ V4() = default;
+  __host__ __device__ __forceinline__ V4(double a, double b, double c, double d) : x(a), y(b), z(c), w(d) {}
+  __host__ __device__ __forceinline__ V4(const V4& o) : x(o.x), y(o.y), z(o.z), w(o.w) {}
+  __host__ __device__ __forceinline__ V4& operator=(const V4& o) {
+    x = o.x;
+    y = o.y;
+    z = o.z;
+    w = o.w;
+    return *this;
+  }
 };
 
 __device__ __forceinline__ V4 vmul(const V4& a, const V4& b) {
@@ -94,68 +127,6 @@ __device__ __forceinline__ V4 vscale(const V4& a, double s) {
 }
 __device__ __forceinline__ double vdot(const V4& a, const V4& b) {
   return fma(a.w, b.w, fma(a.z, b.z, fma(a.y, b.y, a.x * b.x)));
-}
-
-// 16 doubles of a wave-uniform matrix (row-major P[j][k]).  The address is
-// built from SGPR values only, so these become scalar (s_load) loads.
-struct M16 {
-  double m[16];
-};
-__device__ __forceinline__ M16 load_m(const double* __restrict__ p) {
-  M16 r;
-#pragma unroll
-  for (int k = 0; k < 16; ++k) r.m[k] = p[k];
-  return r;
-}
-// P v, summed over k in order (Eigen's unrolled 4x4 product order)
-__device__ __forceinline__ V4 matvec(const M16& M, const V4& v) {
-  V4 r;
-  r.x = fma(M.m[3], v.w, fma(M.m[2], v.z, fma(M.m[1], v.y, M.m[0] * v.x)));
-  r.y = fma(M.m[7], v.w, fma(M.m[6], v.z, fma(M.m[5], v.y, M.m[4] * v.x)));
-  r.z = fma(M.m[11], v.w, fma(M.m[10], v.z, fma(M.m[9], v.y, M.m[8] * v.x)));
-  r.w = fma(M.m[15], v.w, fma(M.m[14], v.z, fma(M.m[13], v.y, M.m[12] * v.x)));
-  return r;
-}
-// P^T v
-__device__ __forceinline__ V4 matTvec(const M16& M, const V4& v) {
-  V4 r;
-  r.x = fma(M.m[12], v.w, fma(M.m[8], v.z, fma(M.m[4], v.y, M.m[0] * v.x)));
-  r.y = fma(M.m[13], v.w, fma(M.m[9], v.z, fma(M.m[5], v.y, M.m[1] * v.x)));
-  r.z = fma(M.m[14], v.w, fma(M.m[10], v.z, fma(M.m[6], v.y, M.m[2] * v.x)));
-  r.w = fma(M.m[15], v.w, fma(M.m[11], v.z, fma(M.m[7], v.y, M.m[3] * v.x)));
-  return r;
-}
-
-// Same products with the matrix read straight from LDS at the point of use
-// (wave-uniform address: broadcast reads), so no 32-VGPR copy stays live.
-__device__ __forceinline__ V4 matvec_p(const double* __restrict__ M, const V4& v) {
-  const double2 m01 = *reinterpret_cast<const double2*>(M + 0), m23 = *reinterpret_cast<const double2*>(M + 2);
-  const double2 m45 = *reinterpret_cast<const double2*>(M + 4), m67 = *reinterpret_cast<const double2*>(M + 6);
-  const double2 m89 = *reinterpret_cast<const double2*>(M + 8), mab = *reinterpret_cast<const double2*>(M + 10);
-  const double2 mcd = *reinterpret_cast<const double2*>(M + 12), mef = *reinterpret_cast<const double2*>(M + 14);
-  V4 r;
-  r.x = fma(m23.y, v.w, fma(m23.x, v.z, fma(m01.y, v.y, m01.x * v.x)));
-  r.y = fma(m67.y, v.w, fma(m67.x, v.z, fma(m45.y, v.y, m45.x * v.x)));
-  r.z = fma(mab.y, v.w, fma(mab.x, v.z, fma(m89.y, v.y, m89.x * v.x)));
-  r.w = fma(mef.y, v.w, fma(mef.x, v.z, fma(mcd.y, v.y, mcd.x * v.x)));
-  return r;
-}
-__device__ __forceinline__ V4 matTvec_p(const double* __restrict__ M, const V4& v) {
-  const double2 m01 = *reinterpret_cast<const double2*>(M + 0), m23 = *reinterpret_cast<const double2*>(M + 2);
-  const double2 m45 = *reinterpret_cast<const double2*>(M + 4), m67 = *reinterpret_cast<const double2*>(M + 6);
-  const double2 m89 = *reinterpret_cast<const double2*>(M + 8), mab = *reinterpret_cast<const double2*>(M + 10);
-  const double2 mcd = *reinterpret_cast<const double2*>(M + 12), mef = *reinterpret_cast<const double2*>(M + 14);
-  V4 r;
-  r.x = fma(mcd.x, v.w, fma(m89.x, v.z, fma(m45.x, v.y, m01.x * v.x)));
-  r.y = fma(mcd.y, v.w, fma(m89.y, v.z, fma(m45.y, v.y, m01.y * v.x)));
-  r.z = fma(mef.x, v.w, fma(mab.x, v.z, fma(m67.x, v.y, m23.x * v.x)));
-  r.w = fma(mef.y, v.w, fma(mab.y, v.z, fma(m67.y, v.y, m23.y * v.x)));
-  return r;
-}
-
-__device__ __forceinline__ V4 tipvec(unsigned code) {
-  return {(double)(code & 1u), (double)((code >> 1) & 1u), (double)((code >> 2) & 1u),
-          (double)((code >> 3) & 1u)};
 }
 
 __device__ __forceinline__ double wave_sum(double v) {
@@ -238,60 +209,36 @@ __device__ __forceinline__ int reduce16_entry(int lane) {
 // kernel arguments
 // ---------------------------------------------------------------------------
 struct SweepArgs {
-  const uint8_t* tips;    // [S][Ppad] state masks
+  const uint8_t* tips;    // [S][Ppad] tip bytes: (state mask << 4) | record vector index
   const double* weights;  // [Ppad]   (0 on padding)
-  const double* pmat;     // [draw][C][nmat][16]  P of every branch, in program-use order
+  const double* pmat;     // [draw][C][nmat][R][4]  matrix records, program-use order
   const double* model;    // [draw][10+2C]
-  double2* scratch;       // [wg][nslots][K][2][C*64]   stored moved partials
-  double* gslot;          // [wg][C][nmat][16]          dL/dP partial sums, program-use order
+  double2* scratch;       // [wg][nslots][K][2][C*64]  stored moved partials
+  double2* dstk;          // [wg][ndeep][K][2][C*64]   deep-stack entries
+  double* gslot;          // [wg][C][nmat][16]  dL/dP partial sums (per-wave atomic adds)
   double* sslot;          // [wg][C][8]
   double* site_ll;        // [draw][P] or null
-  unsigned long long* stamps;  // diagnostic builds (PHY_STAMP): [wg][C][8] s_memtime
   double* out;            // [draw][outlen]: dL/dP rows written in place when g_direct
-  const int* mat_branch;  // [nmat] branch of matrix m (-1: identity)
+  const int* mat_branch;  // [nmat] branch of matrix m
   const double* eig;      // [draw][EIG_LEN] (Q for the chain rule)
   double* inner;          // [draw][C][B] <G, Q P> when g_direct
-  int S, P, Ppad, C, nsteps, nslots, nblk, depth, nmat, cap_m;
+  int S, P, Ppad, C, nsteps, nslots, ndeep, nblk, nmat, R, cap_m;
   int B, outlen, g_direct;  // g_direct: one workgroup per draw
 };
 
-#ifndef PHY_STAMP
-#define PHY_STAMP 0
-#endif
-#ifndef PHY_PF
-#define PHY_PF 1  // reverse-pass prefetch distance (steps): 1 or 2
-#endif
-#define STAMP(k)                                                                      \
-  do {                                                                                \
-    if (PHY_STAMP && a.stamps && blk0 && lane == 0)                                   \
-      a.stamps[((size_t)wg * C + c) * 8 + (k)] = __builtin_amdgcn_s_memtime();         \
-  } while (0)
-
-// LDS carve (all offsets multiples of 16 B), K columns per lane:
-//   P chunk  C * cap_m * 16 double   (matrices [m0, m0+cap_m) of the chunk)
-//   G chunk  C * cap_m * 16 double   (their dL/dP accumulators)
-//   stacks   C waves x max(depth-1, 1) entries x K x 2 x 64 double2 (the
-//            top entry lives in registers); wave c's slice of the root
-//            exchange rootL (K x 64 double) aliases the start of its own
-//            stack, which is empty at the root
-//   tips     S * 64 * K bytes (rounded to 16)
-__host__ __device__ inline size_t wave_stack_bytes(int depth, int K) {
-  return (size_t)(depth > 2 ? depth - 1 : 1) * K * 2 * WAVE * 16;
-}
-__host__ __device__ inline size_t stack_bytes(int C, int depth, int K) {
-  return (size_t)C * wave_stack_bytes(depth, K);
-}
-__host__ __device__ inline size_t lds_bytes(int S, int C, int depth, int cap_m, int K) {
-  size_t b = 2 * (size_t)C * cap_m * 16 * 8;
-  b += stack_bytes(C, depth, K);
-  b += ((size_t)S * WAVE * K + 15) / 16 * 16;
-  return b;
+// LDS carve (16-B aligned pieces), K columns per lane:
+//   tips   S x 64K bytes              shared by the C category waves
+//   rootx  C x K x 64 doubles         root mixture exchange
+//   mats   C x cap_m x R x 4 doubles  wave c's chunk of matrix records
+__host__ __device__ inline size_t tip_lds_bytes(int S, int K) { return ((size_t)S * WAVE * K + 15) / 16 * 16; }
+__host__ __device__ inline size_t lds_bytes(int S, int C, int R, int cap_m, int K) {
+  return tip_lds_bytes(S, K) + (size_t)C * K * WAVE * 8 + (size_t)C * cap_m * R * 32;
 }
 
-// Buffer resource for the workgroup's scratch region: buffer loads past
-// num_records return zeros without touching memory, which lets the reverse
-// pass issue its prefetch unconditionally (tip children get an out-of-range
-// offset) -- no divergent-looking load paths for the waitcnt pass.
+// Buffer resource over a workgroup's scratch / deep-stack region: loads past
+// num_records return zeros without touching memory, so operand prefetches
+// are issued unconditionally (an unused operand gets an out-of-range offset)
+// and the waitcnt pass never sees a load on only one side of a branch.
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* base, uint32_t bytes) {
   const uint64_t a = reinterpret_cast<uint64_t>(base);
   const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)a);
@@ -300,281 +247,172 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* base, ui
   void* p = reinterpret_cast<void*>(((uint64_t)hi << 32) | lo);
   return __builtin_amdgcn_make_buffer_rsrc(p, (short)0, (int)n, 0x00020000);
 }
+// One stored 4-vector: two 16-B halves `half` bytes apart.
+__device__ __forceinline__ V4 ld_v4(__amdgpu_buffer_rsrc_t srd, uint32_t off, uint32_t half) {
+  const auto lo = __builtin_amdgcn_raw_buffer_load_b128(srd, off, 0, 0);
+  const auto hi = __builtin_amdgcn_raw_buffer_load_b128(srd, off + half, 0, 0);
+  V4 r;
+  r.x = __hiloint2double((int)lo[1], (int)lo[0]);
+  r.y = __hiloint2double((int)lo[3], (int)lo[2]);
+  r.z = __hiloint2double((int)hi[1], (int)hi[0]);
+  r.w = __hiloint2double((int)hi[3], (int)hi[2]);
+  return r;
+}
 
 // s_waitcnt vmcnt(0) that the compiler's waitcnt pass sees (an inline-asm
-// wait would be invisible to it): clears loads left pending by staging /
-// flush loops so the step loops are not charged a loop-carried vmcnt(0).
+// wait would be invisible to it): clears loads left pending by staging
+// loops so the step loops are not charged a loop-carried vmcnt(0).
 #define WAIT_VMCNT0() __builtin_amdgcn_s_waitcnt(0x0F70)
 
-// Chunk staging and dL/dP flushes (run at chunk switches only).
-#ifndef PHY_OUTLINE
-#define PHY_OUTLINE 0  // 1: out-of-line calls (measured slower on MI355X)
-#endif
-#if PHY_OUTLINE
-#define PHY_CHUNK_FN __device__ __noinline__
-#else
-#define PHY_CHUNK_FN __device__ __forceinline__
-#endif
-
-// P-matrices [lo, lo+n) of every category -> LDS (one contiguous run of n*16
-// doubles per category, 8 loads in flight per thread before the writes).
-PHY_CHUNK_FN void stage_chunk(double* pl, const double* pmat_d, int C, int cap_m, int nmat, int lo, int n) {
-  const int nthreads = blockDim.x;
-  const int q2 = n * 8;  // double2 per category
-  for (int cc = 0; cc < C; ++cc) {
-    const double2* src = reinterpret_cast<const double2*>(pmat_d + ((size_t)cc * nmat + lo) * 16);
-    double2* dst = reinterpret_cast<double2*>(pl + (size_t)cc * cap_m * 16);
-    for (int k0 = threadIdx.x; k0 < q2; k0 += nthreads * 8) {
-      double2 buf[8];
-#pragma unroll
-      for (int u = 0; u < 8; ++u) {
-        const int k = k0 + u * nthreads;
-        buf[u] = (k < q2) ? src[k] : make_double2(0.0, 0.0);
-      }
-#pragma unroll
-      for (int u = 0; u < 8; ++u) {
-        const int k = k0 + u * nthreads;
-        if (k < q2) dst[k] = buf[u];
-      }
-    }
-  }
-  WAIT_VMCNT0();  // no staging load may look pending inside the step loops
-}
-
-// Hand the LDS dL/dP chunk (matrices [m0, m0+q/16)) to the workgroup's slot
-// and zero it: a plain store the first time (g_first), else load-add-store,
-// contiguous in program order.  With fin (one workgroup per draw, its last
-// pattern block) the totals go to the draw's output rows in branch order
-// and each 16-thread group -- one matrix -- also reduces <G, Q P> into
-// inner[c][b] (the chain rule dP/dt = Q P), from the P chunk still in LDS.
-PHY_CHUNK_FN void flush_chunk(double* gl, const double* pl, double* gslot_wg, double* gout, double* inner_d,
-                              const double* Qd, const int* mat_branch, int C, int cap_m, int nmat, int B, int m0,
-                              int q, bool g_first, bool fin) {
-  const int nthreads = blockDim.x;
-  for (int cc = 0; cc < C; ++cc) {
-    double* gp = gslot_wg + ((size_t)cc * nmat + m0) * 16;
-    double* lp = gl + (size_t)cc * cap_m * 16;
-    const double* pp = pl + (size_t)cc * cap_m * 16;
-    for (int k0 = threadIdx.x; k0 < q; k0 += nthreads * 8) {
-      double old[8];
-#pragma unroll
-      for (int u = 0; u < 8; ++u) {
-        const int k = k0 + u * nthreads;
-        old[u] = (!g_first && k < q) ? gp[k] : 0.0;
-      }
-      if (!fin) {
-#pragma unroll
-        for (int u = 0; u < 8; ++u) {
-          const int k = k0 + u * nthreads;
-          if (k < q) {
-            gp[k] = old[u] + lp[k];
-            lp[k] = 0.0;
-          }
-        }
-        continue;
-      }
-      // 16 consecutive threads hold one matrix (q and the thread count are
-      // multiples of 16), so the groups are uniformly active
-#pragma unroll
-      for (int u = 0; u < 8; ++u) {
-        const int k = k0 + u * nthreads;
-        if (k < q) {
-          const int mm = k >> 4, e16 = k & 15, j = e16 >> 2, kk = e16 & 3;
-          const double g = old[u] + lp[k];
-          lp[k] = 0.0;
-          const int b = mat_branch[m0 + mm];
-          double qp = 0.0;
-#pragma unroll
-          for (int l = 0; l < 4; ++l) qp = fma(Qd[j * 4 + l], pp[mm * 16 + l * 4 + kk], qp);
-          double s = g * qp;
-          s += __shfl_xor(s, 8, 16);
-          s += __shfl_xor(s, 4, 16);
-          s += __shfl_xor(s, 2, 16);
-          s += __shfl_xor(s, 1, 16);
-          if (b >= 0) {
-            gout[((size_t)cc * B + b) * 16 + e16] = g;
-            if (e16 == 0) inner_d[(size_t)cc * B + b] = s;  // dlogL/dt_{b,c}
-          }
-        }
-      }
-    }
-  }
-  WAIT_VMCNT0();
-}
-
-// K mat-vecs sharing one read of the (wave-uniform, LDS-broadcast) matrix.
+// Matrix records (pmat_kernel): R 4-vectors per matrix -- the four columns
+// of P, then P t for every non-one-hot tip mask t present in the data (the
+// reference's tips are one-hot or all-ones, phylostan/utils.py:180-187).
+// A tip child's moved partial P t is therefore one indexed LDS read.
+//   P v   = sum_j col_j v_j   (row i: P_i0 v0 + P_i1 v1 + P_i2 v2 + P_i3 v3)
+//   P^T v = (col_j . v)_j
+// K products share one read of the (wave-uniform: LDS broadcast) columns.
 template <int K>
-__device__ __forceinline__ void matvec_k(const double* __restrict__ M, const V4 (&v)[K], V4 (&r)[K]) {
-  const double2 m01 = *reinterpret_cast<const double2*>(M + 0), m23 = *reinterpret_cast<const double2*>(M + 2);
-  const double2 m45 = *reinterpret_cast<const double2*>(M + 4), m67 = *reinterpret_cast<const double2*>(M + 6);
-  const double2 m89 = *reinterpret_cast<const double2*>(M + 8), mab = *reinterpret_cast<const double2*>(M + 10);
-  const double2 mcd = *reinterpret_cast<const double2*>(M + 12), mef = *reinterpret_cast<const double2*>(M + 14);
+__device__ __forceinline__ void pvec_k(const double* __restrict__ M, const V4 (&v)[K], V4 (&r)[K]) {
+  const double2 a01 = *reinterpret_cast<const double2*>(M + 0), a23 = *reinterpret_cast<const double2*>(M + 2);
+  const double2 b01 = *reinterpret_cast<const double2*>(M + 4), b23 = *reinterpret_cast<const double2*>(M + 6);
+  const double2 c01 = *reinterpret_cast<const double2*>(M + 8), c23 = *reinterpret_cast<const double2*>(M + 10);
+  const double2 d01 = *reinterpret_cast<const double2*>(M + 12), d23 = *reinterpret_cast<const double2*>(M + 14);
 #pragma unroll
   for (int k = 0; k < K; ++k) {
     const V4 x = v[k];
-    r[k].x = fma(m23.y, x.w, fma(m23.x, x.z, fma(m01.y, x.y, m01.x * x.x)));
-    r[k].y = fma(m67.y, x.w, fma(m67.x, x.z, fma(m45.y, x.y, m45.x * x.x)));
-    r[k].z = fma(mab.y, x.w, fma(mab.x, x.z, fma(m89.y, x.y, m89.x * x.x)));
-    r[k].w = fma(mef.y, x.w, fma(mef.x, x.z, fma(mcd.y, x.y, mcd.x * x.x)));
+    r[k].x = fma(d01.x, x.w, fma(c01.x, x.z, fma(b01.x, x.y, a01.x * x.x)));
+    r[k].y = fma(d01.y, x.w, fma(c01.y, x.z, fma(b01.y, x.y, a01.y * x.x)));
+    r[k].z = fma(d23.x, x.w, fma(c23.x, x.z, fma(b23.x, x.y, a23.x * x.x)));
+    r[k].w = fma(d23.y, x.w, fma(c23.y, x.z, fma(b23.y, x.y, a23.y * x.x)));
   }
 }
 template <int K>
-__device__ __forceinline__ void matTvec_k(const double* __restrict__ M, const V4 (&v)[K], V4 (&r)[K]) {
-  const double2 m01 = *reinterpret_cast<const double2*>(M + 0), m23 = *reinterpret_cast<const double2*>(M + 2);
-  const double2 m45 = *reinterpret_cast<const double2*>(M + 4), m67 = *reinterpret_cast<const double2*>(M + 6);
-  const double2 m89 = *reinterpret_cast<const double2*>(M + 8), mab = *reinterpret_cast<const double2*>(M + 10);
-  const double2 mcd = *reinterpret_cast<const double2*>(M + 12), mef = *reinterpret_cast<const double2*>(M + 14);
+__device__ __forceinline__ void ptvec_k(const double* __restrict__ M, const V4 (&v)[K], V4 (&r)[K]) {
+  const double2 a01 = *reinterpret_cast<const double2*>(M + 0), a23 = *reinterpret_cast<const double2*>(M + 2);
+  const double2 b01 = *reinterpret_cast<const double2*>(M + 4), b23 = *reinterpret_cast<const double2*>(M + 6);
+  const double2 c01 = *reinterpret_cast<const double2*>(M + 8), c23 = *reinterpret_cast<const double2*>(M + 10);
+  const double2 d01 = *reinterpret_cast<const double2*>(M + 12), d23 = *reinterpret_cast<const double2*>(M + 14);
 #pragma unroll
   for (int k = 0; k < K; ++k) {
     const V4 x = v[k];
-    r[k].x = fma(mcd.x, x.w, fma(m89.x, x.z, fma(m45.x, x.y, m01.x * x.x)));
-    r[k].y = fma(mcd.y, x.w, fma(m89.y, x.z, fma(m45.y, x.y, m01.y * x.x)));
-    r[k].z = fma(mef.x, x.w, fma(mab.x, x.z, fma(m67.x, x.y, m23.x * x.x)));
-    r[k].w = fma(mef.y, x.w, fma(mab.y, x.z, fma(m67.y, x.y, m23.y * x.x)));
+    r[k].x = fma(a23.y, x.w, fma(a23.x, x.z, fma(a01.y, x.y, a01.x * x.x)));
+    r[k].y = fma(b23.y, x.w, fma(b23.x, x.z, fma(b01.y, x.y, b01.x * x.x)));
+    r[k].z = fma(c23.y, x.w, fma(c23.x, x.z, fma(c01.y, x.y, c01.x * x.x)));
+    r[k].w = fma(d23.y, x.w, fma(d23.x, x.z, fma(d01.y, x.y, d01.x * x.x)));
   }
 }
 
-// `prog`, `chunk_of` and `chunk_m0` are separate __restrict__ const
-// arguments so the backend proves them read-only and uses scalar loads.
+// 0/1 state vector of a tip byte (mask in the high nibble).
+__device__ __forceinline__ V4 tipvec_b(unsigned b) {
+  return {(double)((b >> 4) & 1u), (double)((b >> 5) & 1u), (double)((b >> 6) & 1u), (double)((b >> 7) & 1u)};
+}
+
+// The sweep.  `prog` is a separate __restrict__ const argument so the
+// backend proves it read-only and uses scalar loads.
 //
 // K columns per lane: lane l of the category-c wave owns patterns
 // blk*64K + k*64 + l, k < K.  The columns share every matrix read, the
-// program/stack control flow and -- the main saving -- one wave reduction
-// of the summed outer products per branch.
-// Register budget: two waves per SIMD (<= 256 VGPRs) -- the occupancy the
-// default 80 KiB LDS plan allows.  PHY_WPE overrides it in diagnostic builds.
-#ifndef PHY_WPE
-#define PHY_WPE 2
-#endif
+// program control flow and -- the main saving -- one wave reduction of the
+// summed outer products per branch.
+//
+// Stack discipline of the post-order program (build_program): the operand a
+// step pops is the previous step's result (`top`, in registers) except for
+// the first child x of a node whose children are both internal; those live
+// on a small per-workgroup "deep stack" in global memory (L2-resident),
+// at entries the host assigns statically, and are prefetched one step ahead.
+// The reverse pass mirrors this for the upper partials r.  No LDS stack:
+// LDS holds only tips, the root exchange and the matrix chunks.
+//
+// Register budget: K=2 targets two waves per SIMD (<= 256 VGPRs), K=1 four.
 template <int MAXT, int K>
-__global__ void __launch_bounds__(MAXT) __attribute__((amdgpu_waves_per_eu(PHY_WPE)))
-    sweep_kernel(SweepArgs a, const int* __restrict__ prog, const int* __restrict__ chunk_of,
-                 const int* __restrict__ chunk_m0) {
+__global__ void __launch_bounds__(MAXT) __attribute__((amdgpu_waves_per_eu(K == 2 ? 2 : 4)))
+    sweep_kernel(SweepArgs a, const int* __restrict__ prog) {
   extern __shared__ __attribute__((aligned(16))) unsigned char lds_raw[];
   const int lane = threadIdx.x & (WAVE - 1);
   const int c = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int nthreads = blockDim.x;
   const int draw = blockIdx.y;
   const int wg = blockIdx.y * gridDim.x + blockIdx.x;
-  const int C = a.C, nsteps = a.nsteps, nmat = a.nmat, cap_m = a.cap_m;
+  const int C = a.C, nsteps = a.nsteps, nmat = a.nmat;
+  const int rec = a.R * 4;  // doubles per matrix record
   const int ncolwg = C * WAVE;
-  const bool one_chunk = chunk_of[0] == chunk_of[nsteps - 1];
-  bool blk0 = true;  // first pattern block of this workgroup (diagnostic stamps)
-  if (PHY_STAMP && a.stamps && lane == 0) {
-    a.stamps[((size_t)wg * C + c) * 8 + 6] = __builtin_amdgcn_s_memrealtime();
-    a.stamps[((size_t)wg * C + c) * 8 + 0] = __builtin_amdgcn_s_memtime();
-  }
 
-  double* pl = reinterpret_cast<double*>(lds_raw);  // [C][cap_m][16]
-  double* gl = pl + (size_t)C * cap_m * 16;          // [C][cap_m][16]
-  unsigned char* region = reinterpret_cast<unsigned char*>(gl + (size_t)C * cap_m * 16);
-  const size_t wstk = wave_stack_bytes(a.depth, K);
-  double2* stk = reinterpret_cast<double2*>(region + (size_t)c * wstk);
-  // root exchange: wave cc's K x 64 values at the start of its own stack
-  auto rootL = [&](int cc, int k) -> double* {
-    return reinterpret_cast<double*>(region + (size_t)cc * wstk) + k * WAVE + lane;
-  };
-  unsigned char* tipl = region + stack_bytes(C, a.depth, K);
+  unsigned char* tipl = lds_raw;
+  double* rootx = reinterpret_cast<double*>(lds_raw + tip_lds_bytes(a.S, K));
+  double* mats = rootx + (size_t)C * K * WAVE + (size_t)c * a.cap_m * rec;
 
   const double* mdl = a.model + (size_t)draw * (10 + 2 * C);
   const V4 pi = {mdl[0], mdl[1], mdl[2], mdl[3]};
   const double ps_c = mdl[10 + C + c];
-  const double* pmat_d = a.pmat + (size_t)draw * C * nmat * 16;
-  double2* scr = a.scratch + (size_t)wg * a.nslots * K * 2 * ncolwg;
-  double* gslot_wg = a.gslot + (size_t)wg * C * nmat * 16;
-  const uint32_t scr_bytes = (uint32_t)((size_t)a.nslots * K * 2 * ncolwg * 16);
-  const __amdgpu_buffer_rsrc_t srd = make_rsrc(scr, scr_bytes);
+  const double* pmat_c = a.pmat + ((size_t)draw * C + c) * nmat * rec;
+  const size_t entry2 = (size_t)K * 2 * ncolwg;  // double2 per scratch / deep-stack entry
+  double2* scr = a.scratch + (size_t)wg * a.nslots * entry2;
+  double2* dsk = a.dstk + (size_t)wg * a.ndeep * entry2;
+  const uint32_t scr_bytes = (uint32_t)((size_t)a.nslots * entry2 * 16);
+  const uint32_t dsk_bytes = (uint32_t)((size_t)a.ndeep * entry2 * 16);
+  const __amdgpu_buffer_rsrc_t srd_scr = make_rsrc(scr, scr_bytes);
+  const __amdgpu_buffer_rsrc_t srd_dsk = make_rsrc(dsk, dsk_bytes);
+  const int colw = c * WAVE + lane;  // this lane's column inside an entry half
+  const uint32_t half_bytes = (uint32_t)ncolwg * 16u;
+  auto eoff = [&](int e, int k) __attribute__((always_inline)) -> uint32_t {  // byte offset of (entry, column k), half 0
+    return (uint32_t)((((size_t)e * K + k) * 2 * ncolwg + colw) * 16);
+  };
+  auto put = [&](double2* base, int e, int k, const V4& v) __attribute__((always_inline)) {
+    double2* d = base + ((size_t)e * K + k) * 2 * ncolwg + colw;
+    d[0] = make_double2(v.x, v.y);
+    d[ncolwg] = make_double2(v.z, v.w);
+  };
+
+  // this wave's dL/dP slot: a plain store per (branch, entry) in the
+  // workgroup's first block, then one atomic add per later block, all from
+  // this wave only -- same-address program order, so the sums are bitwise
+  // reproducible and the slot needs no zeroing
+  double* gs = a.gslot + ((size_t)wg * C + c) * nmat * 16;
+  bool gfirst = true;  // wave-uniform
 
   const int e = reduce16_entry(lane);
   const bool gowner = (lane & 3) == 0;
 
-  for (int k = threadIdx.x; k < C * cap_m * 16; k += nthreads) gl[k] = 0.0;
-
   double acc_ll = 0.0, acc_dps = 0.0;
   V4 acc_f = {0.0, 0.0, 0.0, 0.0};
 
-  // ---- P-matrix / dL/dP chunks in LDS ----
-  int cur = -1, m0 = 0, mcount = 0;
-  // Hand the LDS G chunk to this workgroup's global slot and zero it: a
-  // plain store the first time the slot region is written (the workgroup's
-  // first pattern block), otherwise load-add-store, 8 loads in flight per
-  // thread.
-  // Flushes into the workgroup's slot are contiguous (program order).  With
-  // one workgroup per draw (g_direct) the workgroup's LAST flush of each
-  // chunk instead writes the draw's dL/dP output rows (branch order) and
-  // forms the chain-rule inner products <G_cb, Q P_cb> from the P chunk
-  // still in LDS, so the finalize pass never re-reads G or P.
-  bool g_first = true, g_last = false;
-  double* gout = a.out + (size_t)draw * a.outlen + 1 + a.B + 2 * C + 4;
-  const double* Qd = a.eig + (size_t)draw * EIG_LEN + EIG_Q;
-  double* inner_d = a.inner + (size_t)draw * C * a.B;
-  auto flush_g = [&]() {
-    if (cur < 0) return;
-    flush_chunk(gl, pl, gslot_wg, gout, inner_d, Qd, a.mat_branch, C, cap_m, nmat, a.B, m0, mcount * 16,
-                g_first, a.g_direct && g_last);
-  };
-  auto ensure_chunk = [&](int s, bool reverse) {
-    const int ch = chunk_of[s];
-    if (ch == cur) return;  // workgroup-uniform
-    __syncthreads();
-    if (reverse) flush_g();
-    const int lo = chunk_m0[ch], n = chunk_m0[ch + 1] - lo;
-    stage_chunk(pl, pmat_d, C, cap_m, nmat, lo, n);
-    __syncthreads();
+  // ---- this wave's chunk of matrix records in LDS (no barrier: private) ----
+  int cur = -1, m0 = 0;
+  auto ensure_chunk = [&](const int* st) {
+    const int ch = st[ST_CHUNK];
+    if (ch == cur) return;  // wave-uniform
+    const int lo = st[ST_M0], n = st[ST_MN];
+    const double2* src = reinterpret_cast<const double2*>(pmat_c + (size_t)lo * rec);
+    double2* dst = reinterpret_cast<double2*>(mats);
+    const int q2 = n * rec / 2;
+    for (int k0 = lane; k0 < q2; k0 += WAVE * 8) {
+      double2 buf[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int k = k0 + u * WAVE;
+        buf[u] = (k < q2) ? src[k] : make_double2(0.0, 0.0);
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int k = k0 + u * WAVE;
+        if (k < q2) dst[k] = buf[u];
+      }
+    }
+    WAIT_VMCNT0();  // no staging load may look pending inside the step loops
     cur = ch;
     m0 = lo;
-    mcount = n;
   };
-  auto pm = [&](int m) -> const double* { return pl + ((size_t)c * cap_m + (m - m0)) * 16; };
-
-  // Pending-vector stack: the most recent entry stays in registers (most
-  // pushes are popped by the very next step), older ones live in LDS,
-  // [entry][k][half][lane] double2.
-  int sp = 0;
-  bool has_top = false;
-  // top of stack: named scalars (a captured struct or array would be
-  // demoted to scratch)
-  double ta0 = 0.0, ta1 = 0.0, ta2 = 0.0, ta3 = 0.0, tb0 = 0.0, tb1 = 0.0, tb2 = 0.0, tb3 = 0.0;
-  auto spill = [&](int k, double v0, double v1, double v2, double v3) {
-    stk[((sp * K + k) * 2 + 0) * WAVE + lane] = make_double2(v0, v1);
-    stk[((sp * K + k) * 2 + 1) * WAVE + lane] = make_double2(v2, v3);
-  };
-  auto push = [&](const V4 (&v)[K]) {
-    if (has_top) {
-      spill(0, ta0, ta1, ta2, ta3);
-      if constexpr (K == 2) spill(1, tb0, tb1, tb2, tb3);
-      ++sp;
-    }
-    ta0 = v[0].x;
-    ta1 = v[0].y;
-    ta2 = v[0].z;
-    ta3 = v[0].w;
-    if constexpr (K == 2) {
-      tb0 = v[1].x;
-      tb1 = v[1].y;
-      tb2 = v[1].z;
-      tb3 = v[1].w;
-    }
-    has_top = true;
-  };
-  auto pop = [&](V4 (&v)[K]) {
-    if (has_top) {
-      has_top = false;
-      v[0] = {ta0, ta1, ta2, ta3};
-      if constexpr (K == 2) v[1] = {tb0, tb1, tb2, tb3};
-      return;
-    }
-    --sp;
-#pragma unroll
-    for (int k = 0; k < K; ++k) {
-      const double2 lo = stk[((sp * K + k) * 2 + 0) * WAVE + lane];
-      const double2 hi = stk[((sp * K + k) * 2 + 1) * WAVE + lane];
-      v[k] = {lo.x, lo.y, hi.x, hi.y};
-    }
+  auto mrec = [&](int m) __attribute__((always_inline)) -> const double* { return mats + (size_t)(m - m0) * rec; };
+  auto tipb = [&](int t, int k) __attribute__((always_inline)) -> unsigned { return tipl[(t * K + k) * WAVE + lane]; };
+  auto look = [&](int m, unsigned b) __attribute__((always_inline)) -> V4 {  // P t of a tip: one record vector
+    const double* p = mrec(m) + (b & 15u) * 4;
+    const double2 lo = *reinterpret_cast<const double2*>(p);
+    const double2 hi = *reinterpret_cast<const double2*>(p + 2);
+    return {lo.x, lo.y, hi.x, hi.y};
   };
   // dL/dP_m += sum_k r_k (x) p_k, reduced over the wave; the lane owning
-  // entry e adds it to the LDS G chunk (one lane per address).
-  auto gacc = [&](int m, const V4 (&r)[K], const V4 (&p)[K]) {
+  // entry e adds it to this wave's slot.
+  auto gacc = [&](int m, const V4 (&r)[K], const V4 (&p)[K]) __attribute__((always_inline)) {
     double v[16];
     v[0] = r[0].x * p[0].x;  v[1] = r[0].x * p[0].y;  v[2] = r[0].x * p[0].z;  v[3] = r[0].x * p[0].w;
     v[4] = r[0].y * p[0].x;  v[5] = r[0].y * p[0].y;  v[6] = r[0].y * p[0].z;  v[7] = r[0].y * p[0].w;
@@ -591,18 +429,18 @@ __global__ void __launch_bounds__(MAXT) __attribute__((amdgpu_waves_per_eu(PHY_W
       v[12] = fma(r[k].w, p[k].x, v[12]); v[13] = fma(r[k].w, p[k].y, v[13]);
       v[14] = fma(r[k].w, p[k].z, v[14]); v[15] = fma(r[k].w, p[k].w, v[15]);
     }
-    if (PHY_ABLATE & 1) {
-      asm volatile("" ::"v"(v[0]), "v"(v[5]), "v"(v[10]), "v"(v[15]));
-      return;
-    }
     const double sum = reduce16(v, lane);
-    if (gowner) gl[((size_t)c * cap_m + (m - m0)) * 16 + e] += sum;
+    if (gowner) {
+      if (gfirst)
+        gs[(size_t)m * 16 + e] = sum;
+      else
+        unsafeAtomicAdd(gs + (size_t)m * 16 + e, sum);
+    }
   };
-  auto tip_code = [&](int t, int k) -> unsigned { return tipl[(t * K + k) * WAVE + lane]; };
 
   for (int blk = blockIdx.x; blk < a.nblk; blk += gridDim.x) {
-    g_last = blk + (int)gridDim.x >= a.nblk;
-    // stage this block's tip codes in LDS: S rows x 64K bytes, shared by the
+    __syncthreads();  // the previous block's tip / root-exchange reads are done
+    // stage this block's tip bytes in LDS: S rows x 64K bytes, shared by the
     // C category-waves and by both passes (8 loads in flight per thread)
     {
       const uint32_t* src = reinterpret_cast<const uint32_t*>(a.tips);
@@ -627,74 +465,99 @@ __global__ void __launch_bounds__(MAXT) __attribute__((amdgpu_waves_per_eu(PHY_W
     __syncthreads();
     WAIT_VMCNT0();
 
-    STAMP(1);
     // ------------------------------ forward ------------------------------
-    sp = 0;
-    has_top = false;
-    V4 proot[K];
-    for (int s = 0; s < nsteps; ++s) {
-      ensure_chunk(s, false);
-      const int* st = prog + s * STEP_INTS;
-      const int x = st[0], y = st[1], mx = st[2], my = st[3], mv = st[4], vs = st[5], fl = st[6];
-      V4 ax[K], ay[K], pv[K];
-      if (y >= 0) {
-        V4 tv[K];
+    // Step s: a_y = P t_y (tip) or top; a_x = P t_x (tip), top (y a tip) or
+    // the deep operand; p_v = a_x * a_y; a_v = P_v p_v -> scratch slot (and
+    // the deep stack when v is a deep x child); top = a_v.
+    V4 top[K], proot[K];
 #pragma unroll
-        for (int k = 0; k < K; ++k) tv[k] = tipvec(tip_code(y, k));
-        matvec_k<K>(pm(my), tv, ay);
-      } else {
-        pop(ay);
-      }
-      if (x >= 0) {
-        V4 tv[K];
+    for (int k = 0; k < K; ++k) top[k] = proot[k] = {0.0, 0.0, 0.0, 0.0};
+    // dcur: this step's deep operand (loaded one step ahead into dnext,
+    // alternating by name across an unrolled pair of steps: no register
+    // copy of an in-flight load)
+    #define FSTEP(s, dcur, dnext) do {                                                                                \
+      const int* st = prog + s * STEP_INTS;                                                                           \
+      {                                                                                                               \
+        const bool more = s + 1 < nsteps;                                                                             \
+        const int* sn = prog + (more ? s + 1 : s) * STEP_INTS;                                                        \
+        const bool need = more && (sn[ST_FLAGS] & F_XDEEP);                                                           \
+        if (!PHY_FWD_COND || need)                                                                                    \
+      _Pragma("unroll")                                                                                               \
+        for (int k = 0; k < K; ++k) dnext[k] = ld_v4(srd_dsk, need ? eoff(sn[ST_XDPOS], k) : dsk_bytes, half_bytes);  \
+      }                                                                                                               \
+      ensure_chunk(st);                                                                                               \
+      const int x = st[ST_X], y = st[ST_Y], fl = st[ST_FLAGS], vs = st[ST_VSLOT];                                     \
+      V4 ax[K], ay[K], pv[K];                                                                                         \
+      if (y >= 0) {                                                                                                   \
+        const int my = st[ST_MY];                                                                                     \
+      _Pragma("unroll")                                                                                               \
+        for (int k = 0; k < K; ++k) ay[k] = look(my, tipb(y, k));                                                     \
+      } else {                                                                                                        \
+      _Pragma("unroll")                                                                                               \
+        for (int k = 0; k < K; ++k) ay[k] = top[k];                                                                   \
+      }                                                                                                               \
+      if (x >= 0) {                                                                                                   \
+        const int mx = st[ST_MX];                                                                                     \
+      _Pragma("unroll")                                                                                               \
+        for (int k = 0; k < K; ++k) ax[k] = look(mx, tipb(x, k));                                                     \
+      } else if (y >= 0) {                                                                                            \
+      _Pragma("unroll")                                                                                               \
+        for (int k = 0; k < K; ++k) ax[k] = top[k];                                                                   \
+      } else {                                                                                                        \
+      _Pragma("unroll")                                                                                               \
+        for (int k = 0; k < K; ++k) ax[k] = dcur[k];                                                                  \
+      }                                                                                                               \
+      _Pragma("unroll")                                                                                               \
+      for (int k = 0; k < K; ++k) pv[k] = vmul(ax[k], ay[k]);                                                         \
+      if (vs >= 0) {                                                                                                  \
+        V4 av[K];                                                                                                     \
+        if (fl & F_MV) {                                                                                              \
+          pvec_k<K>(mrec(st[ST_MV]), pv, av);                                                                         \
+        } else { /* merged root branch of an unrooted tree: identity */                                                \
+      _Pragma("unroll")                                                                                               \
+          for (int k = 0; k < K; ++k) av[k] = pv[k];                                                                  \
+        }                                                                                                             \
+      _Pragma("unroll")                                                                                               \
+        for (int k = 0; k < K; ++k) if (!(PHY_ABLATE & 8)) put(scr, vs, k, av[k]);                                    \
+        if (fl & F_VDEEP) {                                                                                           \
+          const int dp = st[ST_VDPOS];                                                                                \
+      _Pragma("unroll")                                                                                               \
+          for (int k = 0; k < K; ++k) put(dsk, dp, k, av[k]);                                                         \
+        }                                                                                                             \
+      _Pragma("unroll")                                                                                               \
+        for (int k = 0; k < K; ++k) top[k] = av[k];                                                                   \
+      } else {                                                                                                        \
+      _Pragma("unroll")                                                                                               \
+        for (int k = 0; k < K; ++k) proot[k] = pv[k];                                                                 \
+      }                                                                                                               \
+    } while (0)
+    {
+      V4 dA[K], dB[K];
 #pragma unroll
-        for (int k = 0; k < K; ++k) tv[k] = tipvec(tip_code(x, k));
-        matvec_k<K>(pm(mx), tv, ax);
-      } else {
-        pop(ax);
-      }
-#pragma unroll
-      for (int k = 0; k < K; ++k) pv[k] = vmul(ax[k], ay[k]);
-      if (vs >= 0) {
-        V4 av[K];
-        if (fl & 1) {
-          matvec_k<K>(pm(mv), pv, av);
-        } else {  // merged root branch: identity
-#pragma unroll
-          for (int k = 0; k < K; ++k) av[k] = pv[k];
-        }
-        if (!(PHY_ABLATE & 4)) {
-#pragma unroll
-          for (int k = 0; k < K; ++k) {
-            double2* dst = scr + (size_t)((vs * K + k) * 2) * ncolwg + c * WAVE + lane;
-            dst[0] = make_double2(av[k].x, av[k].y);
-            dst[ncolwg] = make_double2(av[k].z, av[k].w);
-          }
-        }
-        push(av);
-      } else {
-#pragma unroll
-        for (int k = 0; k < K; ++k) proot[k] = pv[k];
+      for (int k = 0; k < K; ++k) dA[k] = {0.0, 0.0, 0.0, 0.0};  // step 0 has no internal child
+      for (int s = 0;;) {
+        FSTEP(s, dA, dB);
+        if (++s >= nsteps) break;
+        FSTEP(s, dB, dA);
+        if (++s >= nsteps) break;
       }
     }
 
-    STAMP(2);
     // ------------------------- root / site log L -------------------------
     double fp[K];
 #pragma unroll
     for (int k = 0; k < K; ++k) {
       fp[k] = vdot(pi, proot[k]);  // pi . p_root,c
-      *rootL(c, k) = ps_c * fp[k];
+      rootx[(c * K + k) * WAVE + lane] = ps_c * fp[k];
     }
     __syncthreads();
     double L[K];
 #pragma unroll
     for (int k = 0; k < K; ++k) {
       L[k] = 0.0;
-      for (int cc = 0; cc < C; ++cc) L[k] += *rootL(cc, k);
+      for (int cc = 0; cc < C; ++cc) L[k] += rootx[(cc * K + k) * WAVE + lane];
     }
-    __syncthreads();  // rootL is stack space again from here on
-    V4 qroot[K];
+    V4 topr[K];
 #pragma unroll
     for (int k = 0; k < K; ++k) {
       const int i = blk * WAVE * K + k * WAVE + lane;  // pattern of this column
@@ -713,140 +576,127 @@ __global__ void __launch_bounds__(MAXT) __attribute__((amdgpu_waves_per_eu(PHY_W
       acc_f.w = fma(s_c, proot[k].w, acc_f.w);
       // upper partials are carried pre-scaled by w_i ps_c / L_i, so every
       // outer product below is already a dlogL/dP term
-      qroot[k] = vscale(pi, s_c);
+      topr[k] = vscale(pi, s_c);
     }
 
-    STAMP(3);
     // ------------------------------ reverse ------------------------------
-    // Upper partials r travel down the stack (the root's q is pushed first;
-    // the root step's own "branch" is the identity).
-    sp = 0;
-    has_top = false;
-    push(qroot);
-    const uint32_t col_off = (uint32_t)((c * WAVE + lane) * 16);
-    auto ld_partial = [&](uint32_t off) -> V4 {
-      const auto lo = __builtin_amdgcn_raw_buffer_load_b128(srd, off, 0, 0);
-      const auto hi = __builtin_amdgcn_raw_buffer_load_b128(srd, off + (uint32_t)ncolwg * 16u, 0, 0);
-      V4 r;
-      r.x = __hiloint2double((int)lo[1], (int)lo[0]);
-      r.y = __hiloint2double((int)lo[3], (int)lo[2]);
-      r.z = __hiloint2double((int)hi[1], (int)hi[0]);
-      r.w = __hiloint2double((int)hi[3], (int)hi[2]);
-      return r;
+    // Step s (program backwards) with upper partial r_v (top, or the deep
+    // stack when v is a deep x child): q_v = P_v^T r_v, r_x = q_v * a_y,
+    // r_y = q_v * a_x, dL/dP_v += r_v (x) (a_x * a_y), and for tip children
+    // dL/dP += r (x) t.  Children's stored a come back from scratch, loaded
+    // one step ahead (zeros for tips: out-of-range offset).
+    struct CSet {
+      V4 lx[K], ly[K], lr[K];
     };
+    #define LOAD_SET(s, r) do {                                                  \
+      const bool ok = s >= 0;                                                    \
+      const int* sp = prog + (ok ? s : 0) * STEP_INTS;                           \
+      const int x = sp[ST_X], y = sp[ST_Y], fl = sp[ST_FLAGS];                   \
+      const bool lx = ok && x < 0, ly = ok && y < 0, lr = ok && (fl & F_VDEEP);  \
+      const int xs = sp[ST_XSLOT], ys = sp[ST_YSLOT], vd = sp[ST_VDPOS];         \
+      _Pragma("unroll")                                                          \
+      for (int k = 0; k < K; ++k) {                                              \
+        r.lx[k] = ld_v4(srd_scr, lx ? eoff(xs, k) : scr_bytes, half_bytes);      \
+        r.ly[k] = ld_v4(srd_scr, ly ? eoff(ys, k) : scr_bytes, half_bytes);      \
+        r.lr[k] = ld_v4(srd_dsk, lr ? eoff(vd, k) : dsk_bytes, half_bytes);      \
+      }                                                                          \
+    } while (0)
+    #define RSTEP(s, cs) do {                                                       \
+      const int* st = prog + s * STEP_INTS;                                         \
+      ensure_chunk(st);                                                             \
+      const int x = st[ST_X], y = st[ST_Y], fl = st[ST_FLAGS];                      \
+      V4 rv[K], ax[K], ay[K], q[K], rx[K], ry[K];                                   \
+      unsigned bx[K], by[K];                                                        \
+      if (fl & F_VDEEP) {                                                           \
+      _Pragma("unroll")                                                             \
+        for (int k = 0; k < K; ++k) rv[k] = cs.lr[k];                               \
+      } else {                                                                      \
+      _Pragma("unroll")                                                             \
+        for (int k = 0; k < K; ++k) rv[k] = topr[k];                                \
+      }                                                                             \
+      if (x >= 0) {                                                                 \
+        const int mx = st[ST_MX];                                                   \
+      _Pragma("unroll")                                                             \
+        for (int k = 0; k < K; ++k) {                                               \
+          bx[k] = tipb(x, k);                                                       \
+          ax[k] = look(mx, bx[k]);                                                  \
+        }                                                                           \
+      } else {                                                                      \
+      _Pragma("unroll")                                                             \
+        for (int k = 0; k < K; ++k) ax[k] = cs.lx[k];                               \
+      }                                                                             \
+      if (y >= 0) {                                                                 \
+        const int my = st[ST_MY];                                                   \
+      _Pragma("unroll")                                                             \
+        for (int k = 0; k < K; ++k) {                                               \
+          by[k] = tipb(y, k);                                                       \
+          ay[k] = look(my, by[k]);                                                  \
+        }                                                                           \
+      } else {                                                                      \
+      _Pragma("unroll")                                                             \
+        for (int k = 0; k < K; ++k) ay[k] = cs.ly[k];                               \
+      }                                                                             \
+      if (fl & F_MV) {                                                              \
+        const int mv = st[ST_MV];                                                   \
+        V4 pv[K];                                                                   \
+      _Pragma("unroll")                                                             \
+        for (int k = 0; k < K; ++k) pv[k] = vmul(ax[k], ay[k]);                     \
+        ptvec_k<K>(mrec(mv), rv, q);                                                \
+        gacc(mv, rv, pv); /* dL/dP_v += r_v (x) p_v */                               \
+      } else { /* root, or the merged root branch: identity */                       \
+      _Pragma("unroll")                                                             \
+        for (int k = 0; k < K; ++k) q[k] = rv[k];                                   \
+      }                                                                             \
+      _Pragma("unroll")                                                             \
+      for (int k = 0; k < K; ++k) {                                                 \
+        rx[k] = vmul(q[k], ay[k]);                                                  \
+        ry[k] = vmul(q[k], ax[k]);                                                  \
+      }                                                                             \
+      if (x >= 0) {                                                                 \
+        V4 tv[K];                                                                   \
+      _Pragma("unroll")                                                             \
+        for (int k = 0; k < K; ++k) tv[k] = tipvec_b(bx[k]);                        \
+        gacc(st[ST_MX], rx, tv);                                                    \
+      }                                                                             \
+      if (y >= 0) {                                                                 \
+        V4 tv[K];                                                                   \
+      _Pragma("unroll")                                                             \
+        for (int k = 0; k < K; ++k) tv[k] = tipvec_b(by[k]);                        \
+        gacc(st[ST_MY], ry, tv);                                                    \
+      }                                                                             \
+      if (x < 0 && y < 0) { /* r_x waits on the deep stack while y's subtree runs */ \
+        const int dp = st[ST_XDPOS];                                                \
+      _Pragma("unroll")                                                             \
+        for (int k = 0; k < K; ++k) {                                               \
+          put(dsk, dp, k, rx[k]);                                                   \
+          topr[k] = ry[k];                                                          \
+        }                                                                           \
+      } else if (y < 0) {                                                           \
+      _Pragma("unroll")                                                             \
+        for (int k = 0; k < K; ++k) topr[k] = ry[k];                                \
+      } else if (x < 0) {                                                           \
+      _Pragma("unroll")                                                             \
+        for (int k = 0; k < K; ++k) topr[k] = rx[k];                                \
+      }                                                                             \
+    } while (0)
     if (!(PHY_ABLATE & 2)) {
-      // The children of step s: codes, stored partials (zeros for tips:
-      // out-of-range buffer offset), tip masks.  Requested PHY_PF steps
-      // ahead into one of PHY_PF+1 register sets that rotate by name (the
-      // loop is unrolled PHY_PF+1 times): no register copy of an in-flight
-      // load, so nothing waits before the data is consumed.
-      struct CSet {
-        int x, y;
-        V4 lx[K], ly[K];
-        unsigned tx[K], ty[K];
-      };
-      auto load_set = [&](int s) -> CSet {
-        CSet r;
-        const int* sp_ = prog + max(s, 0) * STEP_INTS;
-        r.x = (s >= 0) ? sp_[0] : 0;
-        r.y = (s >= 0) ? sp_[1] : 0;
-#pragma unroll
-        for (int k = 0; k < K; ++k) {
-          const uint32_t kx = (s >= 0 && r.x < 0) ? (uint32_t)(((-r.x - 1) * K + k) * 2 * ncolwg) * 16u + col_off
-                                                  : scr_bytes;
-          const uint32_t ky = (s >= 0 && r.y < 0) ? (uint32_t)(((-r.y - 1) * K + k) * 2 * ncolwg) * 16u + col_off
-                                                  : scr_bytes;
-          r.lx[k] = ld_partial(kx);
-          r.ly[k] = ld_partial(ky);
-          r.tx[k] = tip_code(max(r.x, 0), k);
-          r.ty[k] = tip_code(max(r.y, 0), k);
-        }
-        return r;
-      };
-      auto rstep = [&](int s, const CSet& cs) {
-        ensure_chunk(s, true);
-        const int x = cs.x, y = cs.y;
-        const int* st = prog + s * STEP_INTS;
-        const int mx = st[2], my = st[3], mv = st[4], fl = st[6];
-        V4 tvx[K], tvy[K], ax[K], ay[K], rv[K], qv[K];
-#pragma unroll
-        for (int k = 0; k < K; ++k) {
-          tvx[k] = tipvec(cs.tx[k]);
-          tvy[k] = tipvec(cs.ty[k]);
-        }
-        if (x >= 0) {
-          matvec_k<K>(pm(mx), tvx, ax);
-        } else {
-#pragma unroll
-          for (int k = 0; k < K; ++k) ax[k] = cs.lx[k];
-        }
-        if (y >= 0) {
-          matvec_k<K>(pm(my), tvy, ay);
-        } else {
-#pragma unroll
-          for (int k = 0; k < K; ++k) ay[k] = cs.ly[k];
-        }
-        pop(rv);
-        if (fl & 1) {
-          V4 pv[K];
-#pragma unroll
-          for (int k = 0; k < K; ++k) pv[k] = vmul(ax[k], ay[k]);
-          matTvec_k<K>(pm(mv), rv, qv);
-          gacc(mv, rv, pv);  // dL/dP_v += r_v (x) p_v
-        } else {  // root, or the merged root branch: identity
-#pragma unroll
-          for (int k = 0; k < K; ++k) qv[k] = rv[k];
-        }
-        V4 rx[K], ry[K];
-#pragma unroll
-        for (int k = 0; k < K; ++k) {
-          rx[k] = vmul(qv[k], ay[k]);
-          ry[k] = vmul(qv[k], ax[k]);
-        }
-        if (x < 0) push(rx);
-        if (y < 0) push(ry);
-        if (x >= 0) gacc(mx, rx, tvx);
-        if (y >= 0) gacc(my, ry, tvy);
-      };
       int s = nsteps - 1;
-#if PHY_PF >= 2
-      CSet A = load_set(s), Bs = load_set(s - 1), Cs;
+      CSet A, Bs;
+      LOAD_SET(s, A);
       for (;;) {
-        Cs = load_set(s - 2);
-        rstep(s, A);
+        LOAD_SET(s - 1, Bs);
+        RSTEP(s, A);
         if (--s < 0) break;
-        A = load_set(s - 2);
-        rstep(s, Bs);
+        LOAD_SET(s - 1, A);
+        RSTEP(s, Bs);
         if (--s < 0) break;
-        Bs = load_set(s - 2);
-        rstep(s, Cs);
-        if (--s < 0) break;
-      }
-#else
-      CSet A = load_set(s), Bs;
-      for (;;) {
-        Bs = load_set(s - 1);
-        rstep(s, A);
-        if (--s < 0) break;
-        A = load_set(s - 1);
-        rstep(s, Bs);
-        if (--s < 0) break;
-      }
-#endif
-      if (!one_chunk) {  // hand the last chunk's sums to the slot
-        __syncthreads();
-        flush_g();
-        __syncthreads();
-        g_first = false;  // every chunk of the slot has now been written once
       }
     }
     WAIT_VMCNT0();
-    STAMP(4);
-    blk0 = false;
-    __syncthreads();  // tips / rootL are rewritten by the next block
+    gfirst = false;
   }
 
-  // per-workgroup scalar partials: [ll, dps, dfreq0..3]
+  // per-wave scalar partials: [ll, dps, dfreq0..3]
   acc_ll = wave_sum(acc_ll);
   acc_dps = wave_sum(acc_dps);
   acc_f.x = wave_sum(acc_f.x);
@@ -862,14 +712,51 @@ __global__ void __launch_bounds__(MAXT) __attribute__((amdgpu_waves_per_eu(PHY_W
     ss[4] = acc_f.z;
     ss[5] = acc_f.w;
   }
-  if (one_chunk) {  // G accumulated in LDS for the workgroup's lifetime
-    __syncthreads();
-    g_last = true;
-    flush_g();
-  }
-  if (PHY_STAMP && a.stamps && lane == 0) {
-    a.stamps[((size_t)wg * C + c) * 8 + 5] = __builtin_amdgcn_s_memtime();
-    a.stamps[((size_t)wg * C + c) * 8 + 7] = __builtin_amdgcn_s_memrealtime();
+  if (a.g_direct && !(PHY_ABLATE & 4)) {
+    // One workgroup per draw: this wave's slot is the draw's dL/dP for
+    // category c.  Write the output rows (branch order) and the chain-rule
+    // inner products <G_cb, Q P_cb> (dP/dt = Q P), 16 lanes per matrix.
+    // The atomics were performed at L2 once vmcnt drains; the slot is read
+    // back with agent-scope loads (past L1, same XCD's L2).  No device fence:
+    // a release fence here would write back the whole L2 per workgroup.
+    WAIT_VMCNT0();
+    const double* Qd = a.eig + (size_t)draw * EIG_LEN + EIG_Q;
+    double* gout = a.out + (size_t)draw * a.outlen + 1 + a.B + 2 * C + 4;
+    double* inner_d = a.inner + (size_t)draw * C * a.B;
+    // k = lane (mod 64): every item of this lane has the same entry e16 =
+    // (j, kk), so the Q row is loaded once
+    const int e16 = lane & 15, j = e16 >> 2, kk = e16 & 3;
+    const double q0 = Qd[j * 4 + 0], q1 = Qd[j * 4 + 1], q2 = Qd[j * 4 + 2], q3 = Qd[j * 4 + 3];
+    const int tot = nmat * 16;  // a multiple of 16: 16-lane groups are whole
+    constexpr int U = 4;
+    for (int k0 = lane; k0 < tot; k0 += WAVE * U) {
+      double g[U], qp[U];
+      int bb[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {  // all loads in flight before any use
+        const int k = k0 + u * WAVE;
+        const int kc = k < tot ? k : lane;
+        const int mm = kc >> 4;
+        g[u] = __hip_atomic_load(gs + kc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const double2* col = reinterpret_cast<const double2*>(pmat_c + (size_t)mm * rec + kk * 4);  // column kk of P
+        const double2 c01 = col[0], c23 = col[1];
+        qp[u] = fma(q3, c23.y, fma(q2, c23.x, fma(q1, c01.y, q0 * c01.x)));
+        bb[u] = a.mat_branch[mm];
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int k = k0 + u * WAVE;
+        if (k < tot) {
+          double sv = g[u] * qp[u];
+          sv += __shfl_xor(sv, 8, 16);
+          sv += __shfl_xor(sv, 4, 16);
+          sv += __shfl_xor(sv, 2, 16);
+          sv += __shfl_xor(sv, 1, 16);
+          gout[((size_t)c * a.B + bb[u]) * 16 + e16] = g[u];
+          if (e16 == 0) inner_d[(size_t)c * a.B + bb[u]] = sv;
+        }
+      }
+    }
   }
 }
 
@@ -880,10 +767,11 @@ __global__ void __launch_bounds__(MAXT) __attribute__((amdgpu_waves_per_eu(PHY_W
 struct PmatArgs {
   const double* model;    // [draw][10+2C]
   const double* blens;    // [draw][B]
-  const int* mat_branch;  // [nmat] branch (node id) of matrix m, -1 = identity
+  const int* mat_branch;  // [nmat] branch (node id) of matrix m
   double* eig;            // [draw][EIG_LEN]
-  double* pmat;           // [draw][C][nmat][16]  program-use order
-  int C, B, kind, nmat, n;
+  double* pmat;           // [draw][C][nmat][R][4]  records, program-use order
+  int C, B, kind, nmat, n, R;
+  unsigned long long extra;  // tip masks of record vectors 4..R-1, 4 bits each
 };
 
 // Cyclic Jacobi eigendecomposition of a symmetric 4x4 (A overwritten).
@@ -988,7 +876,10 @@ __global__ void __launch_bounds__(64) eig_kernel(PmatArgs a) {
   }
 }
 
-// One thread per (draw, category, matrix): P in program-use order.
+// One thread per (draw, category, matrix): the matrix record in program-use
+// order -- the four columns of P, then P t for each extra tip mask t (the
+// 0/1 sum of P's columns, in column order: bitwise what a mat-vec with the
+// 0/1 vector gives).
 __global__ void __launch_bounds__(256) pmat_kernel(PmatArgs a) {
   __shared__ double e[EIG_LEN];
   const int draw = blockIdx.y;
@@ -999,12 +890,9 @@ __global__ void __launch_bounds__(256) pmat_kernel(PmatArgs a) {
   if (idx >= C * nmat) return;
   const int c = idx / nmat, m = idx - c * nmat;
   const int br = a.mat_branch[m];
-  double2* po = reinterpret_cast<double2*>(a.pmat + (((size_t)draw * C + c) * nmat + m) * 16);
+  double2* po = reinterpret_cast<double2*>(a.pmat + (((size_t)draw * C + c) * nmat + m) * a.R * 4);
   double P[16];
-  if (br < 0) {  // the merged root branch of an unrooted tree (generate_script.py:1019)
-#pragma unroll
-    for (int k = 0; k < 16; ++k) P[k] = (k % 5 == 0) ? 1.0 : 0.0;
-  } else {
+  {
     const double* mdl = a.model + (size_t)draw * (10 + 2 * C);
     const double t = a.blens[(size_t)draw * a.B + br] * mdl[10 + c];
     if (a.kind == PHY_JC69) {  // generate_script.py:765-769
@@ -1028,7 +916,23 @@ __global__ void __launch_bounds__(256) pmat_kernel(PmatArgs a) {
     }
   }
 #pragma unroll
-  for (int k = 0; k < 8; ++k) po[k] = make_double2(P[2 * k], P[2 * k + 1]);
+  for (int j = 0; j < 4; ++j) {  // column j
+    po[2 * j] = make_double2(P[j], P[4 + j]);
+    po[2 * j + 1] = make_double2(P[8 + j], P[12 + j]);
+  }
+  for (int v = 4; v < a.R; ++v) {
+    const unsigned t = (unsigned)(a.extra >> (4 * (v - 4))) & 15u;
+    double r[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      double acc = P[i * 4] * (double)(t & 1u);
+#pragma unroll
+      for (int j = 1; j < 4; ++j) acc = fma(P[i * 4 + j], (double)((t >> j) & 1u), acc);
+      r[i] = acc;
+    }
+    po[2 * v] = make_double2(r[0], r[1]);
+    po[2 * v + 1] = make_double2(r[2], r[3]);
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -1037,14 +941,14 @@ __global__ void __launch_bounds__(256) pmat_kernel(PmatArgs a) {
 struct FinArgs {
   const double* gslot;  // [wg][C][nmat][16]  program-use order
   const double* sslot;  // [wg][C][8]
-  const double* pmat;   // [draw][C][nmat][16]
+  const double* pmat;   // [draw][C][nmat][R][4]  records (columns of P first)
   const double* eig;    // [draw][EIG_LEN]
   const double* blens;  // [draw][B]
   const double* model;  // [draw][10+2C]
   const int* gpos;      // [B] matrix index of branch b
   const double* inner;  // [draw][C][B] <G, Q P> from the sweep when g_direct
   double* out;          // [draw][outlen]
-  int C, B, nmat, gx, outlen, g_direct;
+  int C, B, nmat, gx, outlen, g_direct, R;
 };
 
 // dL/dP of a draw spread over several workgroups: out[draw][og + (c*B+b)*16
@@ -1129,7 +1033,8 @@ __global__ void __launch_bounds__(256) finalize_kernel(FinArgs a) {
     }
   }
   __syncthreads();  // dL/dP rows and Q visible to the whole workgroup
-  const double* pm = a.pmat + (size_t)draw * C * a.nmat * 16;
+  const int rec = a.R * 4;
+  const double* pm = a.pmat + (size_t)draw * C * a.nmat * rec;
   for (int idx = threadIdx.x; idx < C * B; idx += blockDim.x) {
     if (a.g_direct) {  // formed by the sweep's last flush
       inner[idx] = a.inner[(size_t)draw * C * B + idx];
@@ -1137,12 +1042,12 @@ __global__ void __launch_bounds__(256) finalize_kernel(FinArgs a) {
     }
     const int c = idx / B, b = idx - c * B;
     const double* g = out + og + (size_t)idx * 16;
-    const double* P = pm + ((size_t)c * a.nmat + a.gpos[b]) * 16;
+    const double* P = pm + ((size_t)c * a.nmat + a.gpos[b]) * rec;  // column-major
     double gv[16], pv[16];
 #pragma unroll
     for (int k = 0; k < 16; ++k) {
       gv[k] = g[k];
-      pv[k] = P[k];
+      pv[k] = P[(k & 3) * 4 + (k >> 2)];  // row-major P[l][k] = column k, entry l
     }
     double s = 0.0;  // <G, Q P>
 #pragma unroll
@@ -1178,20 +1083,20 @@ __global__ void __launch_bounds__(256) finalize_kernel(FinArgs a) {
 // ---------------------------------------------------------------------------
 struct phy_ctx {
   int S, P, Ppad, C, B, rooted, kind, max_draws, device;
-  int nsteps, nslots, depth, nblk, nmat;
+  int nsteps, nslots, ndeep, nblk, nmat;
+  int R = 5;                     // 4-vectors per matrix record (4 columns + extra tip masks)
+  unsigned long long extra = 0;  // the extra tip masks, 4 bits each
   int wg_budget, cols_pref, wg_cap, lds_budget;
   int cu_count = 256, wg_resident = 512;  // resident workgroups of the current plan
   int K = 1;                   // columns per lane of the current plan
   int cap_m = 0, nchunks = 0;  // current LDS plan
   hipStream_t stream;
-  std::vector<int> prog;  // host copy of the program
+  std::vector<int> prog;  // host copy of the program (chunk fields per plan)
   uint8_t* d_tips = nullptr;
   double* d_w = nullptr;
   int* d_prog = nullptr;
   int* d_gpos = nullptr;
   int* d_mat_branch = nullptr;
-  int* d_chunk_of = nullptr;
-  int* d_chunk_m0 = nullptr;
   double* d_pmat = nullptr;
   double* d_eig = nullptr;
   double* d_inner = nullptr;
@@ -1200,9 +1105,9 @@ struct phy_ctx {
   double* d_out = nullptr;
   double* d_site = nullptr;
   double2* d_scratch = nullptr;
+  double2* d_dstk = nullptr;
   double* d_gslot = nullptr;
   double* d_sslot = nullptr;
-  unsigned long long* d_stamps = nullptr;
   bool timing = false;
   std::vector<hipEvent_t> ev;  // pairs
   int ev_used = 0;
@@ -1217,9 +1122,9 @@ void free_ctx(phy_ctx* c) {
   int dev_old = 0;
   (void)hipGetDevice(&dev_old);
   (void)hipSetDevice(c->device);
-  void* ptrs[] = {c->d_tips,  c->d_w,     c->d_prog,    c->d_gpos,    c->d_mat_branch, c->d_chunk_of,
-                  c->d_chunk_m0, c->d_pmat, c->d_eig, c->d_inner,    c->d_model,   c->d_blens,      c->d_out,
-                  c->d_site,  c->d_scratch, c->d_gslot, c->d_sslot,   c->d_stamps};
+  void* ptrs[] = {c->d_tips,  c->d_w,     c->d_prog,    c->d_gpos,    c->d_mat_branch, c->d_pmat,
+                  c->d_eig,   c->d_inner, c->d_model,   c->d_blens,   c->d_out,        c->d_site,
+                  c->d_scratch, c->d_dstk, c->d_gslot,  c->d_sslot};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   for (hipEvent_t e : c->ev) (void)hipEventDestroy(e);
@@ -1228,11 +1133,19 @@ void free_ctx(phy_ctx* c) {
   delete c;
 }
 
-// Build the traversal program (see DESIGN.md "Traversal program"):
-// post-order with the child needing the deeper stack first, every stored
-// moved partial in a slot, every branch matrix numbered in order of use.
+// Build the traversal program (DESIGN.md "Traversal program"): post-order
+// with the child needing the deeper stack first (Strahler order), every
+// stored moved partial in a slot (its step index), every branch matrix
+// numbered in order of use, and the deep-stack entries.
+//
+// In this post-order the node computed just before v is v's second child y
+// when y is internal, else its first child x when x is internal.  So a step
+// pops `top` (the previous step's result) for y, and for x when y is a tip;
+// only the first child x of a node whose children are both internal waits
+// while y's subtree runs.  Those waits nest, so they live on a stack whose
+// entry per wait is fixed here (ST_XDPOS / ST_VDPOS), used by both passes.
 int build_program(int S, const int32_t* peel, int rooted, std::vector<int>& prog,
-                  std::vector<int>& mat_branch, int& nslots, int& depth) {
+                  std::vector<int>& mat_branch, int& nslots, int& ndeep) {
   const int N = 2 * S - 1;
   std::vector<int> ch1(N, -1), ch2(N, -1);
   std::vector<int> seen(N, 0);
@@ -1261,7 +1174,7 @@ int build_program(int S, const int32_t* peel, int rooted, std::vector<int>& prog
                   "unrooted peel: last row child2 must be node 2S-3 (phylostan.py:264-267)");
     if (merged < S) return fail(PHY_EINVAL, "unrooted peel: node 2S-3 must be internal");
   }
-  // stack need per subtree; larger-need child first (Strahler order)
+  // deep-stack need per subtree; larger-need child first (Strahler order)
   std::vector<int> need(N, 0), first(N, -1), second(N, -1);
   {
     std::vector<int> order;  // post-order of the rooted tree
@@ -1314,54 +1227,64 @@ int build_program(int S, const int32_t* peel, int rooted, std::vector<int>& prog
     }
   }
   if ((int)steps.size() != S - 1) return fail(PHY_EINVAL, "tree is not binary / connected");
-  std::vector<int> slot(N, -1);
-  for (int s = 0; s < S - 1; ++s)
+  std::vector<int> slot(N, -1), parent(N, -1);
+  for (int s = 0; s < S - 1; ++s) {
     if (steps[s] != root) slot[steps[s]] = s;
+    parent[first[steps[s]]] = parent[second[steps[s]]] = steps[s];
+  }
   nslots = S - 2;
   prog.assign((size_t)(S - 1) * STEP_INTS, -1);
   mat_branch.clear();
+  std::vector<int> vdpos(N, -1);
+  int cur = 0;
+  ndeep = 0;
   for (int s = 0; s < S - 1; ++s) {
     const int v = steps[s];
     const int x = first[v], y = second[v];
     int* p = &prog[(size_t)s * STEP_INTS];
-    p[0] = x < S ? x : -(slot[x] + 1);
-    p[1] = y < S ? y : -(slot[y] + 1);
-    p[2] = p[3] = p[4] = -1;
+    p[ST_X] = x < S ? x : -1;
+    p[ST_Y] = y < S ? y : -1;
+    p[ST_MX] = p[ST_MY] = p[ST_MV] = -1;
     if (x < S) {  // tip children: their matrices are used at this step
-      p[2] = (int)mat_branch.size();
+      p[ST_MX] = (int)mat_branch.size();
       mat_branch.push_back(x);
     }
     if (y < S) {
-      p[3] = (int)mat_branch.size();
+      p[ST_MY] = (int)mat_branch.size();
       mat_branch.push_back(y);
     }
-    if (v != root) {  // the step's own branch (identity for the merged one)
-      p[4] = (int)mat_branch.size();
-      mat_branch.push_back(v == merged ? -1 : v);
+    int fl = 0;
+    if (v != root && v != merged) {  // the step's own branch
+      p[ST_MV] = (int)mat_branch.size();
+      mat_branch.push_back(v);
+      fl |= F_MV;
     }
-    p[5] = (v == root) ? -1 : slot[v];
-    p[6] = (v != root && v != merged) ? 1 : 0;
-    p[7] = v;
+    p[ST_VSLOT] = (v == root) ? -1 : slot[v];
+    p[ST_XSLOT] = x >= S ? slot[x] : -1;
+    p[ST_YSLOT] = y >= S ? slot[y] : -1;
+    // operand sources (see the comment above), checked here
+    if (y >= S && (s == 0 || steps[s - 1] != y)) return fail(PHY_EINVAL, "internal: y is not the previous step");
+    if (x >= S && y < S && (s == 0 || steps[s - 1] != x))
+      return fail(PHY_EINVAL, "internal: x is not the previous step");
+    if (x >= S && y >= S) {
+      fl |= F_XDEEP;
+      if (vdpos[x] != cur - 1) return fail(PHY_EINVAL, "internal: deep stack out of order");
+      p[ST_XDPOS] = vdpos[x];
+      --cur;
+    }
+    if (v != root) {
+      const int u = parent[v];
+      if (first[u] == v && second[u] >= S) {  // waits for its sibling's subtree
+        fl |= F_VDEEP;
+        vdpos[v] = cur++;
+        ndeep = std::max(ndeep, cur);
+        p[ST_VDPOS] = vdpos[v];
+      }
+    }
+    p[ST_FLAGS] = fl;
+    p[ST_NODE] = v;
   }
-  // simulate both passes to size the LDS stack exactly
-  int sp = 0, mx = 0;
-  for (int s = 0; s < S - 1; ++s) {
-    const int* p = &prog[(size_t)s * STEP_INTS];
-    if (p[1] < 0) --sp;
-    if (p[0] < 0) --sp;
-    if (sp < 0) return fail(PHY_EINVAL, "internal: forward stack underflow");
-    if (p[5] >= 0) mx = std::max(mx, ++sp);
-  }
-  if (sp != 0) return fail(PHY_EINVAL, "internal: forward stack not empty");
-  for (int s = S - 2; s >= 0; --s) {
-    const int* p = &prog[(size_t)s * STEP_INTS];
-    if (s != S - 2) --sp;
-    if (sp < 0) return fail(PHY_EINVAL, "internal: reverse stack underflow");
-    if (p[0] < 0) mx = std::max(mx, ++sp);
-    if (p[1] < 0) mx = std::max(mx, ++sp);
-  }
-  if (sp != 0) return fail(PHY_EINVAL, "internal: reverse stack not empty");
-  depth = std::max(mx, 1);
+  if (cur != 0) return fail(PHY_EINVAL, "internal: deep stack not empty");
   return PHY_OK;
 }
 
@@ -1376,84 +1299,66 @@ int dalloc(T** p, size_t n) {
 }
 
 constexpr size_t LDS_CAP = 160 * 1024;
-
-constexpr int MIN_CAP_K2 = 24;  // two columns per lane only if chunks stay this large
+constexpr int MIN_CAP = 24;  // an occupancy level is taken only if chunks stay this large
 
 int nblk_for(int P, int K) { return (P + WAVE * K - 1) / (WAVE * K); }
+int waves_per_simd(int K) { return K == 2 ? 2 : 4; }  // the kernel's register budget
 
 // Columns per lane, matrices per LDS chunk and the chunk boundaries over the
-// program.  A plan is (K, LDS budget); a chunk holds >= 3 matrices (one step
-// uses up to three).  With the automatic budget (lds_budget 0) and columns
-// (cols_pref 0) the first plan that keeps chunks of >= MIN_CAP_K2 matrices
-// (or the whole program) wins, in this order (measured on MI355X):
-//   K=2 at 80 KiB (2 workgroups per CU), K=2 at 160 KiB, K=1 at 80 KiB.
+// program.  Occupancy is bounded by registers (two waves per SIMD for K=2,
+// four for K=1) and by LDS; the automatic plan takes the most workgroups
+// per CU whose LDS share still holds chunks of >= MIN_CAP matrices (or the
+// whole program).  An explicit budget (lds_budget) fixes the LDS share.
+// A chunk holds >= 3 matrices (one step uses up to three).
 int plan_chunks(phy_ctx* c) {
-  auto cap_for = [&](int K, size_t budget) {
+  const int K = c->cols_pref ? c->cols_pref : (c->C <= 8 ? 2 : 1);
+  if (K == 2 && c->C > 8) return fail(PHY_EINVAL, "two columns per lane need C <= 8");
+  auto cap_for = [&](size_t budget) {
     int cap = c->nmat;
-    while (cap > 3 && lds_bytes(c->S, c->C, c->depth, cap, K) > budget) --cap;
+    while (cap > 3 && lds_bytes(c->S, c->C, c->R, cap, K) > budget) --cap;
     return cap;
   };
-  auto good = [&](int K, size_t budget) {
-    const int cap = cap_for(K, budget);
-    return lds_bytes(c->S, c->C, c->depth, cap, K) <= budget && cap >= std::min(c->nmat, MIN_CAP_K2);
-  };
-  const size_t dflt = 80 * 1024;
-  // two columns only up to 512-thread workgroups (C <= 8): at 1024 threads
-  // the register budget is 128 VGPRs and the K=2 body would spill
-  int K = (c->C > 8 && c->cols_pref == 0) ? 1 : c->cols_pref;
-  size_t budget = c->lds_budget > 0 ? std::min<size_t>(LDS_CAP, (size_t)c->lds_budget) : 0;
-  if (budget == 0) {
-    if (K == 0) {
-      if (good(2, dflt)) {
-        K = 2, budget = dflt;
-      } else if (good(2, LDS_CAP)) {
-        K = 2, budget = LDS_CAP;
-      } else {
-        K = 1, budget = dflt;
-      }
-    } else {
-      budget = (K == 2 && !good(2, dflt)) ? LDS_CAP : dflt;
+  const int by_waves = std::max(1, 4 * waves_per_simd(K) / c->C);  // workgroups per CU
+  int cap = 0;
+  if (c->lds_budget > 0) {
+    cap = cap_for(std::min<size_t>(LDS_CAP, (size_t)c->lds_budget));
+  } else {
+    for (int t = by_waves; t >= 1; --t) {
+      cap = cap_for(LDS_CAP / t);
+      if (lds_bytes(c->S, c->C, c->R, cap, K) <= LDS_CAP / t && cap >= std::min(c->nmat, MIN_CAP)) break;
     }
-  } else if (K == 0) {
-    K = good(2, budget) ? 2 : 1;
   }
-  const int cap = cap_for(K, budget);
-  if (lds_bytes(c->S, c->C, c->depth, cap, K) > LDS_CAP) return fail(PHY_EINVAL, "tree too deep for LDS");
+  const size_t lds = lds_bytes(c->S, c->C, c->R, cap, K);
+  if (lds > LDS_CAP) return fail(PHY_EINVAL, "tree too large for LDS (tips of one block)");
   c->K = K;
   c->nblk = nblk_for(c->P, K);
-  {
-    // resident workgroups per CU: LDS-limited, and at most two waves per
-    // SIMD (the kernel's register budget), C waves per workgroup
-    const size_t lds = lds_bytes(c->S, c->C, c->depth, cap, K);
-    const int by_lds = (int)std::max<size_t>(1, LDS_CAP / std::max<size_t>(lds, 1));
-    const int by_waves = std::max(1, 8 / c->C);
-    c->wg_resident = c->cu_count * std::min({by_lds, by_waves, 4});
-  }
-  if (cap == c->cap_m && c->d_chunk_of) return PHY_OK;
-  std::vector<int> chunk_of(c->nsteps), m0{0};
-  int used = 0, ch = 0;
+  c->wg_resident = c->cu_count * std::min<int>(by_waves, (int)(LDS_CAP / lds));
+  // chunk boundaries: matrices are numbered in step order, so a chunk is a
+  // run of steps whose matrices fit
+  int used = 0, ch = 0, lo = 0;
+  std::vector<int> first_step{0};
   for (int s = 0; s < c->nsteps; ++s) {
     const int* p = &c->prog[(size_t)s * STEP_INTS];
-    const int n = (p[2] >= 0) + (p[3] >= 0) + (p[4] >= 0);
+    const int n = (p[ST_MX] >= 0) + (p[ST_MY] >= 0) + (p[ST_MV] >= 0);
     if (used + n > cap) {
-      m0.push_back(m0.back() + used);
+      first_step.push_back(s);
+      lo += used;
       used = 0;
       ++ch;
     }
-    chunk_of[s] = ch;
+    int* q = &c->prog[(size_t)s * STEP_INTS];
+    q[ST_CHUNK] = ch;
+    q[ST_M0] = lo;
     used += n;
   }
-  m0.push_back(m0.back() + used);
-  if (m0.back() != c->nmat) return fail(PHY_EINVAL, "internal: chunk plan does not cover the matrices");
-  if (c->d_chunk_of) (void)hipFree(c->d_chunk_of);
-  if (c->d_chunk_m0) (void)hipFree(c->d_chunk_m0);
-  c->d_chunk_of = nullptr;
-  c->d_chunk_m0 = nullptr;
-  int rc = dalloc(&c->d_chunk_of, chunk_of.size());
-  if (!rc) rc = dalloc(&c->d_chunk_m0, m0.size());
-  if (rc) return rc;
-  HIP_TRY(hipMemcpy(c->d_chunk_of, chunk_of.data(), chunk_of.size() * sizeof(int), hipMemcpyHostToDevice));
-  HIP_TRY(hipMemcpy(c->d_chunk_m0, m0.data(), m0.size() * sizeof(int), hipMemcpyHostToDevice));
+  if (lo + used != c->nmat) return fail(PHY_EINVAL, "internal: chunk plan does not cover the matrices");
+  first_step.push_back(c->nsteps);
+  for (int k = 0; k <= ch; ++k) {
+    const int m0 = c->prog[(size_t)first_step[k] * STEP_INTS + ST_M0];
+    const int m1 = (k < ch) ? c->prog[(size_t)first_step[k + 1] * STEP_INTS + ST_M0] : c->nmat;
+    for (int s = first_step[k]; s < first_step[k + 1]; ++s) c->prog[(size_t)s * STEP_INTS + ST_MN] = m1 - m0;
+  }
+  HIP_TRY(hipMemcpy(c->d_prog, c->prog.data(), c->prog.size() * sizeof(int), hipMemcpyHostToDevice));
   c->cap_m = cap;
   c->nchunks = ch + 1;
   return PHY_OK;
@@ -1463,7 +1368,8 @@ int launch(phy_ctx* ctx, int n, const double* d_blens, const double* d_model, do
            double* d_site, hipStream_t st) {
   const int C = ctx->C, B = ctx->B;
   {
-    PmatArgs pa{d_model, d_blens, ctx->d_mat_branch, ctx->d_eig, ctx->d_pmat, C, B, ctx->kind, ctx->nmat, n};
+    PmatArgs pa{d_model, d_blens, ctx->d_mat_branch, ctx->d_eig, ctx->d_pmat, C, B, ctx->kind, ctx->nmat, n,
+                ctx->R, ctx->extra};
     hipLaunchKernelGGL(eig_kernel, dim3((n + 63) / 64), dim3(64), 0, st, pa);
     HIP_TRY(hipGetLastError());
     hipLaunchKernelGGL(pmat_kernel, dim3((C * ctx->nmat + 255) / 256, n), dim3(256), 0, st, pa);
@@ -1473,13 +1379,13 @@ int launch(phy_ctx* ctx, int n, const double* d_blens, const double* d_model, do
   const int budget = ctx->wg_budget > 0 ? ctx->wg_budget : ctx->wg_resident;
   const int gx = std::max(1, std::min(ctx->nblk, (budget + n - 1) / n));
   if ((size_t)gx * n > (size_t)ctx->wg_cap) return fail(PHY_ERANGE, "workgroup cap exceeded");
-  const size_t lds = lds_bytes(ctx->S, C, ctx->depth, ctx->cap_m, ctx->K);
+  const size_t lds = lds_bytes(ctx->S, C, ctx->R, ctx->cap_m, ctx->K);
   const int g_direct = (gx == 1) ? 1 : 0;
-  SweepArgs sa{ctx->d_tips,  ctx->d_w,       ctx->d_pmat,         d_model,     ctx->d_scratch,
-               ctx->d_gslot, ctx->d_sslot,   d_site,              ctx->d_stamps, d_out,
-               ctx->d_mat_branch, ctx->d_eig, ctx->d_inner, ctx->S,    ctx->P,              ctx->Ppad,   C,
-               ctx->nsteps,  ctx->nslots,    ctx->nblk,           ctx->depth,  ctx->nmat,
-               ctx->cap_m,   B,              phy_output_len(ctx), g_direct};
+  SweepArgs sa{ctx->d_tips,  ctx->d_w,     ctx->d_pmat,  d_model,      ctx->d_scratch, ctx->d_dstk,
+               ctx->d_gslot, ctx->d_sslot, d_site,       d_out,        ctx->d_mat_branch, ctx->d_eig,
+               ctx->d_inner, ctx->S,       ctx->P,       ctx->Ppad,    C,              ctx->nsteps,
+               ctx->nslots,  ctx->ndeep,   ctx->nblk,    ctx->nmat,    ctx->R,         ctx->cap_m,
+               B,            phy_output_len(ctx), g_direct};
   hipEvent_t e0 = nullptr, e1 = nullptr;
   if (ctx->timing) {
     if (ctx->ev_used + 2 > (int)ctx->ev.size()) {
@@ -1499,29 +1405,14 @@ int launch(phy_ctx* ctx, int n, const double* d_blens, const double* d_model, do
     HIP_TRY(hipEventRecord(e0, st));
   }
   const int threads = C * WAVE;
-#define PHY_LAUNCH(T, K_)                                                                       \
-  hipLaunchKernelGGL((sweep_kernel<T, K_>), dim3(gx, n), dim3(threads), lds, st, sa, ctx->d_prog, \
-                     ctx->d_chunk_of, ctx->d_chunk_m0)
-  if (ctx->K == 2) {
-    if (threads <= 256)
-      PHY_LAUNCH(256, 2);
-    else if (threads <= 512)
-      PHY_LAUNCH(512, 2);
-    else
-      PHY_LAUNCH(1024, 2);
-  } else {
-    if (threads <= 256)
-      PHY_LAUNCH(256, 1);
-    else if (threads <= 512)
-      PHY_LAUNCH(512, 1);
-    else
-      PHY_LAUNCH(1024, 1);
-  }
-#undef PHY_LAUNCH
+  if (ctx->K == 2)
+    hipLaunchKernelGGL((sweep_kernel<512, 2>), dim3(gx, n), dim3(threads), lds, st, sa, ctx->d_prog);
+  else
+    hipLaunchKernelGGL((sweep_kernel<1024, 1>), dim3(gx, n), dim3(threads), lds, st, sa, ctx->d_prog);
   HIP_TRY(hipGetLastError());
   if (ctx->timing) HIP_TRY(hipEventRecord(e1, st));
   FinArgs fa{ctx->d_gslot, ctx->d_sslot, ctx->d_pmat, ctx->d_eig, d_blens, d_model, ctx->d_gpos, ctx->d_inner, d_out,
-             C,            B,            ctx->nmat,   gx,          phy_output_len(ctx), g_direct};
+             C,            B,            ctx->nmat,   gx,          phy_output_len(ctx), g_direct, ctx->R};
   if (!g_direct) {
     hipLaunchKernelGGL(gsum_kernel, dim3((C * B * 16 + 63) / 64, n), dim3(256), 0, st, fa);
     HIP_TRY(hipGetLastError());
@@ -1568,13 +1459,29 @@ int phy_create(int S, int P, int C, int rooted, int model, const uint8_t* tipcod
   c->Ppad = nblk_for(P, 2) * 2 * WAVE;  // room for either column plan
   c->stream = nullptr;
   std::vector<int> mat_branch;
-  int rc = build_program(S, peel, c->rooted, c->prog, mat_branch, c->nslots, c->depth);
+  int rc = build_program(S, peel, c->rooted, c->prog, mat_branch, c->nslots, c->ndeep);
   if (rc) {
     delete c;
     return rc;
   }
   c->nsteps = S - 1;
   c->nmat = (int)mat_branch.size();
+  // matrix records: 4 columns + P t for every non-one-hot mask t in the data
+  // (15 always: the padding patterns' mask)
+  std::vector<int> vec_of(16, -1);
+  {
+    bool present[16] = {false};
+    for (size_t k = 0; k < (size_t)S * P; ++k) present[tipcodes[k]] = true;
+    present[15] = true;
+    for (int j = 0; j < 4; ++j) vec_of[1 << j] = j;
+    int R = 4;
+    for (int t = 0; t < 16; ++t)
+      if (present[t] && vec_of[t] < 0) {
+        c->extra |= (unsigned long long)t << (4 * (R - 4));
+        vec_of[t] = R++;
+      }
+    c->R = R;
+  }
   c->cols_pref = 0;
   {
     const char* lb = getenv("PHY_LDS_BUDGET");
@@ -1600,14 +1507,12 @@ int phy_create(int S, int P, int C, int rooted, int model, const uint8_t* tipcod
   // gfx950: one workgroup may use the whole 160 KiB LDS; dynamic LDS above
   // 64 KiB has to be opted into per kernel.
   {
-    const void* ks[] = {(const void*)sweep_kernel<256, 1>, (const void*)sweep_kernel<512, 1>,
-                        (const void*)sweep_kernel<1024, 1>, (const void*)sweep_kernel<256, 2>,
-                        (const void*)sweep_kernel<512, 2>, (const void*)sweep_kernel<1024, 2>};
+    const void* ks[] = {(const void*)sweep_kernel<1024, 1>, (const void*)sweep_kernel<512, 2>};
     for (const void* k : ks) (void)hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)LDS_CAP);
   }
-  if (lds_bytes(S, C, c->depth, 3, 1) > LDS_CAP) {
+  if (lds_bytes(S, C, c->R, 3, 1) > LDS_CAP) {
     delete c;
-    return fail(PHY_EINVAL, "tree too deep for the LDS stack");
+    return fail(PHY_EINVAL, "too many taxa for one block's tips in LDS");
   }
 #define TRY_C(expr)              \
   do {                           \
@@ -1634,7 +1539,7 @@ int phy_create(int S, int P, int C, int rooted, int model, const uint8_t* tipcod
   TRY_C(dalloc(&c->d_prog, c->prog.size()));
   TRY_C(dalloc(&c->d_mat_branch, (size_t)c->nmat));
   TRY_C(dalloc(&c->d_gpos, (size_t)c->B));
-  TRY_C(dalloc(&c->d_pmat, (size_t)max_draws * C * c->nmat * 16));
+  TRY_C(dalloc(&c->d_pmat, (size_t)max_draws * C * c->nmat * c->R * 4));
   TRY_C(dalloc(&c->d_eig, (size_t)max_draws * EIG_LEN));
   TRY_C(dalloc(&c->d_inner, (size_t)max_draws * C * c->B));
   TRY_C(dalloc(&c->d_model, (size_t)max_draws * (10 + 2 * C)));
@@ -1642,17 +1547,25 @@ int phy_create(int S, int P, int C, int rooted, int model, const uint8_t* tipcod
   TRY_C(dalloc(&c->d_out, (size_t)max_draws * phy_output_len(c)));
   TRY_C(dalloc(&c->d_site, (size_t)max_draws * P));
   TRY_C(dalloc(&c->d_scratch, (size_t)c->wg_cap * std::max(c->nslots, 1) * 2 * 2 * ncolwg));
+  TRY_C(dalloc(&c->d_dstk, (size_t)c->wg_cap * std::max(c->ndeep, 1) * 2 * 2 * ncolwg));
   TRY_C(dalloc(&c->d_gslot, (size_t)c->wg_cap * C * c->nmat * 16));
   TRY_C(dalloc(&c->d_sslot, (size_t)c->wg_cap * C * 8));
-  if (PHY_STAMP) TRY_C(dalloc(&c->d_stamps, (size_t)c->wg_cap * C * 8));
   {
-    std::vector<uint8_t> tips((size_t)S * c->Ppad, 15);
-    for (int t = 0; t < S; ++t) std::memcpy(&tips[(size_t)t * c->Ppad], tipcodes + (size_t)t * P, P);
+    // tip bytes: (mask << 4) | record vector of the mask; padding = mask 15
+    std::vector<uint8_t> tips((size_t)S * c->Ppad, (uint8_t)((15 << 4) | vec_of[15]));
+    for (int t = 0; t < S; ++t)
+      for (int i = 0; i < P; ++i) {
+        const int m = tipcodes[(size_t)t * P + i];
+        tips[(size_t)t * c->Ppad + i] = (uint8_t)((m << 4) | vec_of[m]);
+      }
     std::vector<double> w(c->Ppad, 0.0);
     std::memcpy(w.data(), weights, sizeof(double) * P);
     std::vector<int> gpos(c->B, -1);
-    for (int m = 0; m < c->nmat; ++m)
-      if (mat_branch[m] >= 0) gpos[mat_branch[m]] = m;
+    if (c->nmat != c->B) {
+      free_ctx(c);
+      return fail(PHY_EINVAL, "internal: one matrix per branch expected");
+    }
+    for (int m = 0; m < c->nmat; ++m) gpos[mat_branch[m]] = m;
     for (int b = 0; b < c->B; ++b)
       if (gpos[b] < 0) {
         std::string m_ = "internal: branch " + std::to_string(b) + " not in the program";
@@ -1685,7 +1598,7 @@ int phy_program_info(const phy_ctx* ctx, int* nsteps, int* nslots, int* depth, i
   if (!ctx) return fail(PHY_EINVAL, "NULL ctx");
   if (nsteps) *nsteps = ctx->nsteps;
   if (nslots) *nslots = ctx->nslots;
-  if (depth) *depth = ctx->depth;
+  if (depth) *depth = ctx->ndeep;
   if (nblocks) *nblocks = ctx->nblk;
   return PHY_OK;
 }
@@ -1784,24 +1697,13 @@ int phy_set_tuning(phy_ctx* ctx, int wg_budget, int cols, int lds_budget) {
   return plan_chunks(ctx);
 }
 
-// Diagnostic builds (-DPHY_STAMP=1): copy the per-wave s_memtime stamps of
-// the last launch ([wg][C][8]: start, fwd, root, rev, end-of-block, end,
-// realtime start, realtime end).  Returns the number of values copied.
-int phy_debug_stamps(phy_ctx* ctx, unsigned long long* out, int n) {
-  if (!ctx || !ctx->d_stamps) return 0;
-  const int m = std::min(n, ctx->wg_cap * ctx->C * 8);
-  if (hipMemcpy(out, ctx->d_stamps, sizeof(unsigned long long) * m, hipMemcpyDeviceToHost) != hipSuccess)
-    return 0;
-  return m;
-}
-
 int phy_columns_per_lane(const phy_ctx* ctx) { return ctx ? ctx->K : -1; }
 
-int phy_lds_plan(const phy_ctx* ctx, int* g_in_lds, int* chunk_steps, int* lds_bytes_out) {
+int phy_lds_plan(const phy_ctx* ctx, int* n_chunks, int* matrices_per_chunk, int* lds_bytes_out) {
   if (!ctx) return fail(PHY_EINVAL, "NULL ctx");
-  if (g_in_lds) *g_in_lds = ctx->nchunks;  // number of P / dL/dP chunks per pass
-  if (chunk_steps) *chunk_steps = ctx->cap_m;
-  if (lds_bytes_out) *lds_bytes_out = (int)lds_bytes(ctx->S, ctx->C, ctx->depth, ctx->cap_m, ctx->K);
+  if (n_chunks) *n_chunks = ctx->nchunks;  // matrix-record chunks per pass
+  if (matrices_per_chunk) *matrices_per_chunk = ctx->cap_m;
+  if (lds_bytes_out) *lds_bytes_out = (int)lds_bytes(ctx->S, ctx->C, ctx->R, ctx->cap_m, ctx->K);
   return PHY_OK;
 }
 
