@@ -144,6 +144,14 @@ int phy_lds_plan(const phy_ctx* ctx, int* n_chunks, int* matrices_per_chunk, int
 /* Pattern columns each lane carries in the current plan (1 or 2). */
 int phy_columns_per_lane(const phy_ctx* ctx);
 
+/* Where the sweep keeps its deep stack (operands that wait while a sibling
+ * subtree runs): 0 = automatic (LDS when it fits beside matrix chunks of
+ * >= 24 at the plan's occupancy, else the global per-workgroup region),
+ * 1 = LDS, 2 = global.  Replans; PHY_DEEP sets the default at phy_create.
+ * phy_deep_stack_in_lds reports the current plan (1 LDS, 0 global). */
+int phy_set_deep_stack(phy_ctx* ctx, int mode);
+int phy_deep_stack_in_lds(const phy_ctx* ctx);
+
 #ifdef __cplusplus
 }
 #endif

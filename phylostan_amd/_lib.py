@@ -41,6 +41,8 @@ SIGNATURES = {
     "phy_set_tuning": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int]),
     "phy_lds_plan": (ctypes.c_int, [ctypes.c_void_p, _c_int_p, _c_int_p, _c_int_p]),
     "phy_columns_per_lane": (ctypes.c_int, [ctypes.c_void_p]),
+    "phy_set_deep_stack": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
+    "phy_deep_stack_in_lds": (ctypes.c_int, [ctypes.c_void_p]),
 }
 
 

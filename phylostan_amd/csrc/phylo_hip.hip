@@ -231,8 +231,10 @@ struct SweepArgs {
 //   rootx  C x K x 64 doubles         root mixture exchange
 //   mats   C x cap_m x R x 4 doubles  wave c's chunk of matrix records
 __host__ __device__ inline size_t tip_lds_bytes(int S, int K) { return ((size_t)S * WAVE * K + 15) / 16 * 16; }
-__host__ __device__ inline size_t lds_bytes(int S, int C, int R, int cap_m, int K) {
-  return tip_lds_bytes(S, K) + (size_t)C * K * WAVE * 8 + (size_t)C * cap_m * R * 32;
+//   deep   C x ndl x K x 2 x 64 double2 (ndl = ndeep when the deep stack is in LDS, else 0)
+__host__ __device__ inline size_t lds_bytes(int S, int C, int R, int cap_m, int K, int ndl) {
+  return tip_lds_bytes(S, K) + (size_t)C * K * WAVE * 8 + (size_t)C * cap_m * R * 32 +
+         (size_t)C * ndl * K * 2 * WAVE * 16;
 }
 
 // Buffer resource over a workgroup's scratch / deep-stack region: loads past
@@ -324,7 +326,9 @@ __device__ __forceinline__ V4 tipvec_b(unsigned b) {
 // LDS holds only tips, the root exchange and the matrix chunks.
 //
 // Register budget: K=2 targets two waves per SIMD (<= 256 VGPRs), K=1 four.
-template <int MAXT, int K>
+// DL: the deep stack lives in LDS (no VMEM traffic or prefetch for it),
+// else in the per-workgroup global region behind a buffer descriptor.
+template <int MAXT, int K, bool DL>
 __global__ void __launch_bounds__(MAXT) __attribute__((amdgpu_waves_per_eu(K == 2 ? 2 : 4)))
     sweep_kernel(SweepArgs a, const int* __restrict__ prog) {
   extern __shared__ __attribute__((aligned(16))) unsigned char lds_raw[];
@@ -361,6 +365,19 @@ __global__ void __launch_bounds__(MAXT) __attribute__((amdgpu_waves_per_eu(K == 
     double2* d = base + ((size_t)e * K + k) * 2 * ncolwg + colw;
     d[0] = make_double2(v.x, v.y);
     d[ncolwg] = make_double2(v.z, v.w);
+  };
+  // LDS deep stack (DL): this wave's ndeep x K x 2 halves x 64 double2
+  double2* dlw = reinterpret_cast<double2*>(rootx + (size_t)C * K * WAVE + (size_t)C * a.cap_m * rec) +
+                 (size_t)c * a.ndeep * K * 2 * WAVE;
+  auto dput = [&](int e, int k, const V4& v) __attribute__((always_inline)) {
+    double2* d = dlw + (size_t)(e * K + k) * 2 * WAVE + lane;
+    d[0] = make_double2(v.x, v.y);
+    d[WAVE] = make_double2(v.z, v.w);
+  };
+  auto dget = [&](int e, int k) __attribute__((always_inline)) -> V4 {
+    const double2* d = dlw + (size_t)(e * K + k) * 2 * WAVE + lane;
+    const double2 lo = d[0], hi = d[WAVE];
+    return V4(lo.x, lo.y, hi.x, hi.y);
   };
 
   // this wave's dL/dP slot: a plain store per (branch, entry) in the
@@ -481,7 +498,7 @@ __global__ void __launch_bounds__(MAXT) __attribute__((amdgpu_waves_per_eu(K == 
         const bool more = s + 1 < nsteps;                                                                             \
         const int* sn = prog + (more ? s + 1 : s) * STEP_INTS;                                                        \
         const bool need = more && (sn[ST_FLAGS] & F_XDEEP);                                                           \
-        if (!PHY_FWD_COND || need)                                                                                    \
+        if (!DL && (!PHY_FWD_COND || need))                                                                           \
       _Pragma("unroll")                                                                                               \
         for (int k = 0; k < K; ++k) dnext[k] = ld_v4(srd_dsk, need ? eoff(sn[ST_XDPOS], k) : dsk_bytes, half_bytes);  \
       }                                                                                                               \
@@ -505,7 +522,7 @@ __global__ void __launch_bounds__(MAXT) __attribute__((amdgpu_waves_per_eu(K == 
         for (int k = 0; k < K; ++k) ax[k] = top[k];                                                                   \
       } else {                                                                                                        \
       _Pragma("unroll")                                                                                               \
-        for (int k = 0; k < K; ++k) ax[k] = dcur[k];                                                                  \
+        for (int k = 0; k < K; ++k) ax[k] = DL ? dget(st[ST_XDPOS], k) : dcur[k];                                     \
       }                                                                                                               \
       _Pragma("unroll")                                                                                               \
       for (int k = 0; k < K; ++k) pv[k] = vmul(ax[k], ay[k]);                                                         \
@@ -522,7 +539,9 @@ __global__ void __launch_bounds__(MAXT) __attribute__((amdgpu_waves_per_eu(K == 
         if (fl & F_VDEEP) {                                                                                           \
           const int dp = st[ST_VDPOS];                                                                                \
       _Pragma("unroll")                                                                                               \
-          for (int k = 0; k < K; ++k) put(dsk, dp, k, av[k]);                                                         \
+          for (int k = 0; k < K; ++k) {                                                                               \
+            if constexpr (DL) dput(dp, k, av[k]); else put(dsk, dp, k, av[k]);                                        \
+          }                                                                                                           \
         }                                                                                                             \
       _Pragma("unroll")                                                                                               \
         for (int k = 0; k < K; ++k) top[k] = av[k];                                                                   \
@@ -598,7 +617,8 @@ __global__ void __launch_bounds__(MAXT) __attribute__((amdgpu_waves_per_eu(K == 
       for (int k = 0; k < K; ++k) {                                              \
         r.lx[k] = ld_v4(srd_scr, lx ? eoff(xs, k) : scr_bytes, half_bytes);      \
         r.ly[k] = ld_v4(srd_scr, ly ? eoff(ys, k) : scr_bytes, half_bytes);      \
-        r.lr[k] = ld_v4(srd_dsk, lr ? eoff(vd, k) : dsk_bytes, half_bytes);      \
+        if constexpr (!DL)                                                       \
+          r.lr[k] = ld_v4(srd_dsk, lr ? eoff(vd, k) : dsk_bytes, half_bytes);    \
       }                                                                          \
     } while (0)
     #define RSTEP(s, cs) do {                                                       \
@@ -609,7 +629,7 @@ __global__ void __launch_bounds__(MAXT) __attribute__((amdgpu_waves_per_eu(K == 
       unsigned bx[K], by[K];                                                        \
       if (fl & F_VDEEP) {                                                           \
       _Pragma("unroll")                                                             \
-        for (int k = 0; k < K; ++k) rv[k] = cs.lr[k];                               \
+        for (int k = 0; k < K; ++k) rv[k] = DL ? dget(st[ST_VDPOS], k) : cs.lr[k];  \
       } else {                                                                      \
       _Pragma("unroll")                                                             \
         for (int k = 0; k < K; ++k) rv[k] = topr[k];                                \
@@ -668,7 +688,7 @@ __global__ void __launch_bounds__(MAXT) __attribute__((amdgpu_waves_per_eu(K == 
         const int dp = st[ST_XDPOS];                                                \
       _Pragma("unroll")                                                             \
         for (int k = 0; k < K; ++k) {                                               \
-          put(dsk, dp, k, rx[k]);                                                   \
+          if constexpr (DL) dput(dp, k, rx[k]); else put(dsk, dp, k, rx[k]);        \
           topr[k] = ry[k];                                                          \
         }                                                                           \
       } else if (y < 0) {                                                           \
@@ -1090,6 +1110,8 @@ struct phy_ctx {
   int cu_count = 256, wg_resident = 512;  // resident workgroups of the current plan
   int K = 1;                   // columns per lane of the current plan
   int cap_m = 0, nchunks = 0;  // current LDS plan
+  int deep_pref = 0;           // deep stack: 0 automatic, 1 LDS, 2 global
+  bool deep_lds = false;       // current plan keeps the deep stack in LDS
   hipStream_t stream;
   std::vector<int> prog;  // host copy of the program (chunk fields per plan)
   uint8_t* d_tips = nullptr;
@@ -1313,22 +1335,43 @@ int waves_per_simd(int K) { return K == 2 ? 2 : 4; }  // the kernel's register b
 int plan_chunks(phy_ctx* c) {
   const int K = c->cols_pref ? c->cols_pref : (c->C <= 8 ? 2 : 1);
   if (K == 2 && c->C > 8) return fail(PHY_EINVAL, "two columns per lane need C <= 8");
+  int ndl = 0;  // deep-stack entries held in LDS
   auto cap_for = [&](size_t budget) {
     int cap = c->nmat;
-    while (cap > 3 && lds_bytes(c->S, c->C, c->R, cap, K) > budget) --cap;
+    while (cap > 3 && lds_bytes(c->S, c->C, c->R, cap, K, ndl) > budget) --cap;
     return cap;
+  };
+  auto fits = [&](int cap, size_t budget) {
+    return lds_bytes(c->S, c->C, c->R, cap, K, ndl) <= budget && cap >= std::min(c->nmat, MIN_CAP);
   };
   const int by_waves = std::max(1, 4 * waves_per_simd(K) / c->C);  // workgroups per CU
   int cap = 0;
   if (c->lds_budget > 0) {
-    cap = cap_for(std::min<size_t>(LDS_CAP, (size_t)c->lds_budget));
+    const size_t budget = std::min<size_t>(LDS_CAP, (size_t)c->lds_budget);
+    if (c->deep_pref != 2) {  // LDS deep stack if it leaves chunks of MIN_CAP (or is forced)
+      ndl = c->ndeep;
+      cap = cap_for(budget);
+      if (c->deep_pref == 0 && !fits(cap, budget)) ndl = 0;
+    }
+    if (ndl == 0) cap = cap_for(budget);
   } else {
+    // most workgroups per CU first; at each level the LDS deep stack when
+    // it fits beside chunks of MIN_CAP, else the global one
     for (int t = by_waves; t >= 1; --t) {
-      cap = cap_for(LDS_CAP / t);
-      if (lds_bytes(c->S, c->C, c->R, cap, K) <= LDS_CAP / t && cap >= std::min(c->nmat, MIN_CAP)) break;
+      const size_t budget = LDS_CAP / t;
+      if (c->deep_pref != 2) {
+        ndl = c->ndeep;
+        cap = cap_for(budget);
+        if (fits(cap, budget) || (c->deep_pref == 1 && t == 1)) break;
+      }
+      if (c->deep_pref != 1) {
+        ndl = 0;
+        cap = cap_for(budget);
+        if (fits(cap, budget)) break;
+      }
     }
   }
-  const size_t lds = lds_bytes(c->S, c->C, c->R, cap, K);
+  const size_t lds = lds_bytes(c->S, c->C, c->R, cap, K, ndl);
   if (lds > LDS_CAP) return fail(PHY_EINVAL, "tree too large for LDS (tips of one block)");
   c->K = K;
   c->nblk = nblk_for(c->P, K);
@@ -1361,6 +1404,7 @@ int plan_chunks(phy_ctx* c) {
   HIP_TRY(hipMemcpy(c->d_prog, c->prog.data(), c->prog.size() * sizeof(int), hipMemcpyHostToDevice));
   c->cap_m = cap;
   c->nchunks = ch + 1;
+  c->deep_lds = ndl > 0;
   return PHY_OK;
 }
 
@@ -1379,7 +1423,7 @@ int launch(phy_ctx* ctx, int n, const double* d_blens, const double* d_model, do
   const int budget = ctx->wg_budget > 0 ? ctx->wg_budget : ctx->wg_resident;
   const int gx = std::max(1, std::min(ctx->nblk, (budget + n - 1) / n));
   if ((size_t)gx * n > (size_t)ctx->wg_cap) return fail(PHY_ERANGE, "workgroup cap exceeded");
-  const size_t lds = lds_bytes(ctx->S, C, ctx->R, ctx->cap_m, ctx->K);
+  const size_t lds = lds_bytes(ctx->S, C, ctx->R, ctx->cap_m, ctx->K, ctx->deep_lds ? ctx->ndeep : 0);
   const int g_direct = (gx == 1) ? 1 : 0;
   SweepArgs sa{ctx->d_tips,  ctx->d_w,     ctx->d_pmat,  d_model,      ctx->d_scratch, ctx->d_dstk,
                ctx->d_gslot, ctx->d_sslot, d_site,       d_out,        ctx->d_mat_branch, ctx->d_eig,
@@ -1406,9 +1450,15 @@ int launch(phy_ctx* ctx, int n, const double* d_blens, const double* d_model, do
   }
   const int threads = C * WAVE;
   if (ctx->K == 2)
-    hipLaunchKernelGGL((sweep_kernel<512, 2>), dim3(gx, n), dim3(threads), lds, st, sa, ctx->d_prog);
+    if (ctx->deep_lds)
+      hipLaunchKernelGGL((sweep_kernel<512, 2, true>), dim3(gx, n), dim3(threads), lds, st, sa, ctx->d_prog);
+    else
+      hipLaunchKernelGGL((sweep_kernel<512, 2, false>), dim3(gx, n), dim3(threads), lds, st, sa, ctx->d_prog);
   else
-    hipLaunchKernelGGL((sweep_kernel<1024, 1>), dim3(gx, n), dim3(threads), lds, st, sa, ctx->d_prog);
+    if (ctx->deep_lds)
+      hipLaunchKernelGGL((sweep_kernel<1024, 1, true>), dim3(gx, n), dim3(threads), lds, st, sa, ctx->d_prog);
+    else
+      hipLaunchKernelGGL((sweep_kernel<1024, 1, false>), dim3(gx, n), dim3(threads), lds, st, sa, ctx->d_prog);
   HIP_TRY(hipGetLastError());
   if (ctx->timing) HIP_TRY(hipEventRecord(e1, st));
   FinArgs fa{ctx->d_gslot, ctx->d_sslot, ctx->d_pmat, ctx->d_eig, d_blens, d_model, ctx->d_gpos, ctx->d_inner, d_out,
@@ -1490,6 +1540,8 @@ int phy_create(int S, int P, int C, int rooted, int model, const uint8_t* tipcod
     c->wg_budget = env ? std::max(1, atoi(env)) : 0;  // 0: resident workgroups of the plan
     const char* ck = getenv("PHY_COLS");
     c->cols_pref = ck ? std::max(0, std::min(2, atoi(ck))) : 0;
+    const char* dk = getenv("PHY_DEEP");
+    c->deep_pref = dk ? std::max(0, std::min(2, atoi(dk))) : 0;
   }
   hipError_t he = hipSetDevice(device);
   if (he != hipSuccess) {
@@ -1507,10 +1559,11 @@ int phy_create(int S, int P, int C, int rooted, int model, const uint8_t* tipcod
   // gfx950: one workgroup may use the whole 160 KiB LDS; dynamic LDS above
   // 64 KiB has to be opted into per kernel.
   {
-    const void* ks[] = {(const void*)sweep_kernel<1024, 1>, (const void*)sweep_kernel<512, 2>};
+    const void* ks[] = {(const void*)sweep_kernel<1024, 1, false>, (const void*)sweep_kernel<512, 2, false>,
+                        (const void*)sweep_kernel<1024, 1, true>, (const void*)sweep_kernel<512, 2, true>};
     for (const void* k : ks) (void)hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)LDS_CAP);
   }
-  if (lds_bytes(S, C, c->R, 3, 1) > LDS_CAP) {
+  if (lds_bytes(S, C, c->R, 3, 1, 0) > LDS_CAP) {
     delete c;
     return fail(PHY_EINVAL, "too many taxa for one block's tips in LDS");
   }
@@ -1699,11 +1752,21 @@ int phy_set_tuning(phy_ctx* ctx, int wg_budget, int cols, int lds_budget) {
 
 int phy_columns_per_lane(const phy_ctx* ctx) { return ctx ? ctx->K : -1; }
 
+int phy_set_deep_stack(phy_ctx* ctx, int mode) {
+  if (!ctx) return fail(PHY_EINVAL, "NULL ctx");
+  if (mode < 0 || mode > 2) return fail(PHY_EINVAL, "deep-stack mode must be 0 (automatic), 1 (LDS) or 2 (global)");
+  ctx->deep_pref = mode;
+  HIP_TRY(hipSetDevice(ctx->device));
+  return plan_chunks(ctx);
+}
+int phy_deep_stack_in_lds(const phy_ctx* ctx) { return ctx ? (ctx->deep_lds ? 1 : 0) : -1; }
+
 int phy_lds_plan(const phy_ctx* ctx, int* n_chunks, int* matrices_per_chunk, int* lds_bytes_out) {
   if (!ctx) return fail(PHY_EINVAL, "NULL ctx");
   if (n_chunks) *n_chunks = ctx->nchunks;  // matrix-record chunks per pass
   if (matrices_per_chunk) *matrices_per_chunk = ctx->cap_m;
-  if (lds_bytes_out) *lds_bytes_out = (int)lds_bytes(ctx->S, ctx->C, ctx->R, ctx->cap_m, ctx->K);
+  if (lds_bytes_out)
+    *lds_bytes_out = (int)lds_bytes(ctx->S, ctx->C, ctx->R, ctx->cap_m, ctx->K, ctx->deep_lds ? ctx->ndeep : 0);
   return PHY_OK;
 }
 

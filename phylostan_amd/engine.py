@@ -161,11 +161,16 @@ class TreeLikelihood:
         _lib.check(self.lib.phy_set_tuning(self.ctx, int(wg_budget), int(cols), int(lds_budget)),
                    "phy_set_tuning")
 
+    def set_deep_stack(self, mode=0):
+        """Deep-stack placement: 0 automatic, 1 LDS, 2 global (replans)."""
+        _lib.check(self.lib.phy_set_deep_stack(self.ctx, int(mode)), "phy_set_deep_stack")
+
     def lds_plan(self):
         vals = [ctypes.c_int() for _ in range(3)]
         _lib.check(self.lib.phy_lds_plan(self.ctx, *[ctypes.byref(v) for v in vals]), "phy_lds_plan")
         out = dict(zip(("n_chunks", "matrices_per_chunk", "lds_bytes"), [v.value for v in vals]))
         out["cols"] = self.lib.phy_columns_per_lane(self.ctx)
+        out["deep_lds"] = self.lib.phy_deep_stack_in_lds(self.ctx)
         return out
 
     def timing_start(self):

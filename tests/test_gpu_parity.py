@@ -99,6 +99,24 @@ def test_lds_plans(lds_budget, chunks):
     check_case(case, eng)
 
 
+@pytest.mark.parametrize("mode", [1, 2], ids=["deep_lds", "deep_global"])
+@pytest.mark.parametrize("cols", [1, 2])
+@pytest.mark.parametrize("seed,S,P,C,model,rooted,cat,wg", [
+    (41, 40, 300, 2, "GTR", True, False, 0),       # random topology: several deep entries
+    (42, 128, 200, 4, "HKY", True, False, 3),      # synthetic-config taxa, persistent loop
+    (43, 33, 140, 4, "GTR", False, False, 0),      # unrooted
+])
+def test_deep_stack_placement(mode, cols, seed, S, P, C, model, rooted, cat, wg):
+    """The deep stack (operands waiting while a sibling subtree runs) in LDS
+    or in the per-workgroup global region gives the oracle's answers."""
+    case = cases.random_case(seed, S=S, P=P, C=C, model=model, rooted=rooted, caterpillar=cat)
+    eng = _engine(case)
+    eng.set_tuning(wg, cols, 0)
+    eng.set_deep_stack(mode)
+    assert eng.lds_plan()["deep_lds"] == (1 if mode == 1 else 0)
+    check_case(case, eng)
+
+
 @pytest.mark.parametrize("cols", [1, 2])
 @pytest.mark.parametrize("seed,S,P,C,model,rooted,cat,lds", [
     (31, 12, 130, 4, "HKY", True, False, 0),       # ragged: 130 = 128 + 2
