@@ -93,9 +93,10 @@ def synthetic_problem(sites):
 def algorithmic_bytes(S, P, C, nslots, B, draws):
     """HBM bytes one sweep launch must move (DESIGN.md "Roofline"):
     every non-root internal partial written once + read once (2 x 32 B per
-    slot per column), tip codes (S B/pattern), weights (8 B/pattern),
-    P-matrices in + dL/dP out (2 x 128 B per branch-category)."""
-    per_draw = 64 * nslots * C * P + S * P + 8 * P + 256 * B * C
+    slot per column), tip codes (S/2 B/pattern: 4-bit record indices),
+    weights (8 B/pattern), P-matrices in + dL/dP out (2 x 128 B per
+    branch-category)."""
+    per_draw = 64 * nslots * C * P + S * P // 2 + 8 * P + 256 * B * C
     return per_draw * draws
 
 

@@ -145,10 +145,12 @@ int phy_lds_plan(const phy_ctx* ctx, int* n_chunks, int* matrices_per_chunk, int
 int phy_columns_per_lane(const phy_ctx* ctx);
 
 /* Where the sweep keeps its deep stack (operands that wait while a sibling
- * subtree runs): 0 = automatic (LDS when it fits beside matrix chunks of
- * >= 24 at the plan's occupancy, else the global per-workgroup region),
- * 1 = LDS, 2 = global.  Replans; PHY_DEEP sets the default at phy_create.
- * phy_deep_stack_in_lds reports the current plan (1 LDS, 0 global). */
+ * subtree runs; phy_program_info's `depth` entries): 0 = automatic (all of
+ * it in LDS when that leaves matrix chunks of >= 24 at the plan's
+ * occupancy, else its outermost entries in LDS and the rest in the global
+ * per-workgroup region), 1 = LDS, 2 = global.  Replans; PHY_DEEP sets the
+ * default at phy_create.  phy_deep_stack_in_lds returns how many entries
+ * the current plan holds in LDS. */
 int phy_set_deep_stack(phy_ctx* ctx, int mode);
 int phy_deep_stack_in_lds(const phy_ctx* ctx);
 

@@ -209,7 +209,7 @@ __device__ __forceinline__ int reduce16_entry(int lane) {
 // kernel arguments
 // ---------------------------------------------------------------------------
 struct SweepArgs {
-  const uint8_t* tips;    // [S][Ppad] tip bytes: (state mask << 4) | record vector index
+  const uint8_t* tips;    // [S][Ppad/2] tip nibbles: record vector index, pattern 2j+1 in the high nibble
   const double* weights;  // [Ppad]   (0 on padding)
   const double* pmat;     // [draw][C][nmat][R][4]  matrix records, program-use order
   const double* model;    // [draw][10+2C]
@@ -222,19 +222,24 @@ struct SweepArgs {
   const int* mat_branch;  // [nmat] branch of matrix m
   const double* eig;      // [draw][EIG_LEN] (Q for the chain rule)
   double* inner;          // [draw][C][B] <G, Q P> when g_direct
-  int S, P, Ppad, C, nsteps, nslots, ndeep, nblk, nmat, R, cap_m;
+  int S, P, Ppad, C, nsteps, nslots, ndeep, ndl, nblk, nmat, R, cap_m;  // ndl: deep entries in LDS
   int B, outlen, g_direct;  // g_direct: one workgroup per draw
+  unsigned long long extra;  // tip masks of record vectors 4..R-1, 4 bits each
 };
 
 // LDS carve (16-B aligned pieces), K columns per lane:
-//   tips   S x 64K bytes              shared by the C category waves
-//   rootx  C x K x 64 doubles         root mixture exchange
+//   tips   S x 64K nibbles            record indices, shared by the C category waves
 //   mats   C x cap_m x R x 4 doubles  wave c's chunk of matrix records
-__host__ __device__ inline size_t tip_lds_bytes(int S, int K) { return ((size_t)S * WAVE * K + 15) / 16 * 16; }
-//   deep   C x ndl x K x 2 x 64 double2 (ndl = ndeep when the deep stack is in LDS, else 0)
+//   tail   per wave: ndl deep entries of K x 2 x 64 double2 (the deep
+//          entries [0, ndl) kept in LDS), or K x 64 doubles when ndl = 0;
+//          wave c's root-exchange slice (K x 64 doubles) sits at the start
+//          of its own tail, whose deep entries are all free at the root
+__host__ __device__ inline size_t tip_lds_bytes(int S, int K) { return ((size_t)S * WAVE * K / 2 + 15) / 16 * 16; }
+__host__ __device__ inline size_t tail_doubles(int K, int ndl) {  // per wave
+  return ndl > 0 ? (size_t)ndl * K * 2 * WAVE * 2 : (size_t)K * WAVE;
+}
 __host__ __device__ inline size_t lds_bytes(int S, int C, int R, int cap_m, int K, int ndl) {
-  return tip_lds_bytes(S, K) + (size_t)C * K * WAVE * 8 + (size_t)C * cap_m * R * 32 +
-         (size_t)C * ndl * K * 2 * WAVE * 16;
+  return tip_lds_bytes(S, K) + (size_t)C * cap_m * R * 32 + (size_t)C * tail_doubles(K, ndl) * 8;
 }
 
 // Buffer resource over a workgroup's scratch / deep-stack region: loads past
@@ -304,9 +309,11 @@ __device__ __forceinline__ void ptvec_k(const double* __restrict__ M, const V4 (
   }
 }
 
-// 0/1 state vector of a tip byte (mask in the high nibble).
-__device__ __forceinline__ V4 tipvec_b(unsigned b) {
-  return {(double)((b >> 4) & 1u), (double)((b >> 5) & 1u), (double)((b >> 6) & 1u), (double)((b >> 7) & 1u)};
+// 0/1 state vector of a tip's record index b: the one-hot columns 0..3, then
+// the extra masks (4 bits each in `extra`).
+__device__ __forceinline__ V4 tipvec_b(unsigned b, unsigned long long extra) {
+  const unsigned m = b < 4 ? (1u << b) : (unsigned)(extra >> (4 * (b - 4))) & 15u;
+  return {(double)(m & 1u), (double)((m >> 1) & 1u), (double)((m >> 2) & 1u), (double)((m >> 3) & 1u)};
 }
 
 // The sweep.  `prog` is a separate __restrict__ const argument so the
@@ -342,8 +349,11 @@ __global__ void __launch_bounds__(MAXT) __attribute__((amdgpu_waves_per_eu(K == 
   const int ncolwg = C * WAVE;
 
   unsigned char* tipl = lds_raw;
-  double* rootx = reinterpret_cast<double*>(lds_raw + tip_lds_bytes(a.S, K));
-  double* mats = rootx + (size_t)C * K * WAVE + (size_t)c * a.cap_m * rec;
+  double* mats0 = reinterpret_cast<double*>(lds_raw + tip_lds_bytes(a.S, K));
+  double* mats = mats0 + (size_t)c * a.cap_m * rec;
+  const int ndl = DL ? a.ndeep : a.ndl;  // deep entries [0, ndl) live in LDS
+  double* tail0 = mats0 + (size_t)C * a.cap_m * rec;
+  const size_t tstride = tail_doubles(K, ndl);
 
   const double* mdl = a.model + (size_t)draw * (10 + 2 * C);
   const V4 pi = {mdl[0], mdl[1], mdl[2], mdl[3]};
@@ -366,9 +376,8 @@ __global__ void __launch_bounds__(MAXT) __attribute__((amdgpu_waves_per_eu(K == 
     d[0] = make_double2(v.x, v.y);
     d[ncolwg] = make_double2(v.z, v.w);
   };
-  // LDS deep stack (DL): this wave's ndeep x K x 2 halves x 64 double2
-  double2* dlw = reinterpret_cast<double2*>(rootx + (size_t)C * K * WAVE + (size_t)C * a.cap_m * rec) +
-                 (size_t)c * a.ndeep * K * 2 * WAVE;
+  // this wave's LDS deep entries: ndl x K x 2 halves x 64 double2
+  double2* dlw = reinterpret_cast<double2*>(tail0 + (size_t)c * tstride);
   auto dput = [&](int e, int k, const V4& v) __attribute__((always_inline)) {
     double2* d = dlw + (size_t)(e * K + k) * 2 * WAVE + lane;
     d[0] = make_double2(v.x, v.y);
@@ -420,7 +429,10 @@ __global__ void __launch_bounds__(MAXT) __attribute__((amdgpu_waves_per_eu(K == 
     m0 = lo;
   };
   auto mrec = [&](int m) __attribute__((always_inline)) -> const double* { return mats + (size_t)(m - m0) * rec; };
-  auto tipb = [&](int t, int k) __attribute__((always_inline)) -> unsigned { return tipl[(t * K + k) * WAVE + lane]; };
+  // record index of tip t, column k: a nibble (two lanes share a byte)
+  auto tipb = [&](int t, int k) __attribute__((always_inline)) -> unsigned {
+    return (tipl[(t * K + k) * (WAVE / 2) + (lane >> 1)] >> ((lane & 1) * 4)) & 15u;
+  };
   auto look = [&](int m, unsigned b) __attribute__((always_inline)) -> V4 {  // P t of a tip: one record vector
     const double* p = mrec(m) + (b & 15u) * 4;
     const double2 lo = *reinterpret_cast<const double2*>(p);
@@ -462,8 +474,8 @@ __global__ void __launch_bounds__(MAXT) __attribute__((amdgpu_waves_per_eu(K == 
     {
       const uint32_t* src = reinterpret_cast<const uint32_t*>(a.tips);
       uint32_t* dst = reinterpret_cast<uint32_t*>(tipl);
-      const int rowq = a.Ppad / 4;
-      constexpr int wq = WAVE * K / 4;  // words per tip row
+      const int rowq = a.Ppad / 8;
+      constexpr int wq = WAVE * K / 8;  // words per tip row of this block
       const int nq = a.S * wq;
       for (int k0 = threadIdx.x; k0 < nq; k0 += nthreads * 8) {
         uint32_t buf[8];
@@ -497,10 +509,11 @@ __global__ void __launch_bounds__(MAXT) __attribute__((amdgpu_waves_per_eu(K == 
       {                                                                                                               \
         const bool more = s + 1 < nsteps;                                                                             \
         const int* sn = prog + (more ? s + 1 : s) * STEP_INTS;                                                        \
-        const bool need = more && (sn[ST_FLAGS] & F_XDEEP);                                                           \
-        if (!DL && (!PHY_FWD_COND || need))                                                                           \
+        /* an x operand whose deep entry is global is read back from x's scratch slot */                              \
+        const bool need = more && (sn[ST_FLAGS] & F_XDEEP) && sn[ST_XDPOS] >= ndl;                                    \
+        if (!DL)                                                                                                      \
       _Pragma("unroll")                                                                                               \
-        for (int k = 0; k < K; ++k) dnext[k] = ld_v4(srd_dsk, need ? eoff(sn[ST_XDPOS], k) : dsk_bytes, half_bytes);  \
+        for (int k = 0; k < K; ++k) dnext[k] = ld_v4(srd_scr, need ? eoff(sn[ST_XSLOT], k) : scr_bytes, half_bytes);  \
       }                                                                                                               \
       ensure_chunk(st);                                                                                               \
       const int x = st[ST_X], y = st[ST_Y], fl = st[ST_FLAGS], vs = st[ST_VSLOT];                                     \
@@ -521,8 +534,16 @@ __global__ void __launch_bounds__(MAXT) __attribute__((amdgpu_waves_per_eu(K == 
       _Pragma("unroll")                                                                                               \
         for (int k = 0; k < K; ++k) ax[k] = top[k];                                                                   \
       } else {                                                                                                        \
+        {                                                                                                             \
+          const int xd = st[ST_XDPOS];                                                                                \
+          if (DL || xd < ndl) {                                                                                       \
       _Pragma("unroll")                                                                                               \
-        for (int k = 0; k < K; ++k) ax[k] = DL ? dget(st[ST_XDPOS], k) : dcur[k];                                     \
+            for (int k = 0; k < K; ++k) ax[k] = dget(xd, k);                                                          \
+          } else {                                                                                                    \
+      _Pragma("unroll")                                                                                               \
+            for (int k = 0; k < K; ++k) ax[k] = dcur[k];                                                              \
+          }                                                                                                           \
+        }                                                                                                             \
       }                                                                                                               \
       _Pragma("unroll")                                                                                               \
       for (int k = 0; k < K; ++k) pv[k] = vmul(ax[k], ay[k]);                                                         \
@@ -538,10 +559,8 @@ __global__ void __launch_bounds__(MAXT) __attribute__((amdgpu_waves_per_eu(K == 
         for (int k = 0; k < K; ++k) if (!(PHY_ABLATE & 8)) put(scr, vs, k, av[k]);                                    \
         if (fl & F_VDEEP) {                                                                                           \
           const int dp = st[ST_VDPOS];                                                                                \
-      _Pragma("unroll")                                                                                               \
-          for (int k = 0; k < K; ++k) {                                                                               \
-            if constexpr (DL) dput(dp, k, av[k]); else put(dsk, dp, k, av[k]);                                        \
-          }                                                                                                           \
+          if (DL || dp < ndl)  /* a global entry is x's scratch slot itself */                                        \
+          for (int k = 0; k < K; ++k) dput(dp, k, av[k]);                                                             \
         }                                                                                                             \
       _Pragma("unroll")                                                                                               \
         for (int k = 0; k < K; ++k) top[k] = av[k];                                                                   \
@@ -567,15 +586,16 @@ __global__ void __launch_bounds__(MAXT) __attribute__((amdgpu_waves_per_eu(K == 
 #pragma unroll
     for (int k = 0; k < K; ++k) {
       fp[k] = vdot(pi, proot[k]);  // pi . p_root,c
-      rootx[(c * K + k) * WAVE + lane] = ps_c * fp[k];
+      tail0[(size_t)c * tstride + k * WAVE + lane] = ps_c * fp[k];
     }
     __syncthreads();
     double L[K];
 #pragma unroll
     for (int k = 0; k < K; ++k) {
       L[k] = 0.0;
-      for (int cc = 0; cc < C; ++cc) L[k] += rootx[(cc * K + k) * WAVE + lane];
+      for (int cc = 0; cc < C; ++cc) L[k] += tail0[(size_t)cc * tstride + k * WAVE + lane];
     }
+    __syncthreads();  // every wave has read the exchange before deep entries are rewritten
     V4 topr[K];
 #pragma unroll
     for (int k = 0; k < K; ++k) {
@@ -611,7 +631,8 @@ __global__ void __launch_bounds__(MAXT) __attribute__((amdgpu_waves_per_eu(K == 
       const bool ok = s >= 0;                                                    \
       const int* sp = prog + (ok ? s : 0) * STEP_INTS;                           \
       const int x = sp[ST_X], y = sp[ST_Y], fl = sp[ST_FLAGS];                   \
-      const bool lx = ok && x < 0, ly = ok && y < 0, lr = ok && (fl & F_VDEEP);  \
+      const bool lx = ok && x < 0, ly = ok && y < 0;                             \
+      const bool lr = ok && (fl & F_VDEEP) && sp[ST_VDPOS] >= ndl;               \
       const int xs = sp[ST_XSLOT], ys = sp[ST_YSLOT], vd = sp[ST_VDPOS];         \
       _Pragma("unroll")                                                          \
       for (int k = 0; k < K; ++k) {                                              \
@@ -628,8 +649,14 @@ __global__ void __launch_bounds__(MAXT) __attribute__((amdgpu_waves_per_eu(K == 
       V4 rv[K], ax[K], ay[K], q[K], rx[K], ry[K];                                   \
       unsigned bx[K], by[K];                                                        \
       if (fl & F_VDEEP) {                                                           \
+        const int vd = st[ST_VDPOS];                                                \
+        if (DL || vd < ndl) {                                                       \
       _Pragma("unroll")                                                             \
-        for (int k = 0; k < K; ++k) rv[k] = DL ? dget(st[ST_VDPOS], k) : cs.lr[k];  \
+          for (int k = 0; k < K; ++k) rv[k] = dget(vd, k);                          \
+        } else {                                                                    \
+      _Pragma("unroll")                                                             \
+          for (int k = 0; k < K; ++k) rv[k] = cs.lr[k];                             \
+        }                                                                           \
       } else {                                                                      \
       _Pragma("unroll")                                                             \
         for (int k = 0; k < K; ++k) rv[k] = topr[k];                                \
@@ -675,20 +702,20 @@ __global__ void __launch_bounds__(MAXT) __attribute__((amdgpu_waves_per_eu(K == 
       if (x >= 0) {                                                                 \
         V4 tv[K];                                                                   \
       _Pragma("unroll")                                                             \
-        for (int k = 0; k < K; ++k) tv[k] = tipvec_b(bx[k]);                        \
+        for (int k = 0; k < K; ++k) tv[k] = tipvec_b(bx[k], a.extra);                        \
         gacc(st[ST_MX], rx, tv);                                                    \
       }                                                                             \
       if (y >= 0) {                                                                 \
         V4 tv[K];                                                                   \
       _Pragma("unroll")                                                             \
-        for (int k = 0; k < K; ++k) tv[k] = tipvec_b(by[k]);                        \
+        for (int k = 0; k < K; ++k) tv[k] = tipvec_b(by[k], a.extra);                        \
         gacc(st[ST_MY], ry, tv);                                                    \
       }                                                                             \
       if (x < 0 && y < 0) { /* r_x waits on the deep stack while y's subtree runs */ \
         const int dp = st[ST_XDPOS];                                                \
       _Pragma("unroll")                                                             \
         for (int k = 0; k < K; ++k) {                                               \
-          if constexpr (DL) dput(dp, k, rx[k]); else put(dsk, dp, k, rx[k]);        \
+          if (DL || dp < ndl) dput(dp, k, rx[k]); else put(dsk, dp, k, rx[k]);  \
           topr[k] = ry[k];                                                          \
         }                                                                           \
       } else if (y < 0) {                                                           \
@@ -1111,7 +1138,8 @@ struct phy_ctx {
   int K = 1;                   // columns per lane of the current plan
   int cap_m = 0, nchunks = 0;  // current LDS plan
   int deep_pref = 0;           // deep stack: 0 automatic, 1 LDS, 2 global
-  bool deep_lds = false;       // current plan keeps the deep stack in LDS
+  bool deep_lds = false;       // current plan keeps the whole deep stack in LDS
+  int ndl = 0;                 // deep entries in LDS (== ndeep when deep_lds)
   hipStream_t stream;
   std::vector<int> prog;  // host copy of the program (chunk fields per plan)
   uint8_t* d_tips = nullptr;
@@ -1346,30 +1374,32 @@ int plan_chunks(phy_ctx* c) {
   };
   const int by_waves = std::max(1, 4 * waves_per_simd(K) / c->C);  // workgroups per CU
   int cap = 0;
-  if (c->lds_budget > 0) {
-    const size_t budget = std::min<size_t>(LDS_CAP, (size_t)c->lds_budget);
-    if (c->deep_pref != 2) {  // LDS deep stack if it leaves chunks of MIN_CAP (or is forced)
+  // Deep-stack placement at a given LDS share: the whole stack in LDS if it
+  // fits beside chunks of MIN_CAP matrices (mode 0/1), else (mode 0/2) its
+  // outermost entries [0, ndl) in LDS and the rest in global memory, with
+  // the largest ndl that still fits.
+  auto place = [&](size_t budget, bool last) -> bool {
+    if (c->deep_pref != 2) {
       ndl = c->ndeep;
       cap = cap_for(budget);
-      if (c->deep_pref == 0 && !fits(cap, budget)) ndl = 0;
+      if (fits(cap, budget) || (c->deep_pref == 1 && last)) return true;
+      if (c->deep_pref == 1) return false;
     }
-    if (ndl == 0) cap = cap_for(budget);
+    for (ndl = c->ndeep - 1; ndl >= 0; --ndl) {
+      if (c->deep_pref == 2) ndl = 0;
+      cap = cap_for(budget);
+      if (fits(cap, budget)) return true;
+    }
+    ndl = 0;
+    cap = cap_for(budget);
+    return false;
+  };
+  if (c->lds_budget > 0) {
+    place(std::min<size_t>(LDS_CAP, (size_t)c->lds_budget), true);
   } else {
-    // most workgroups per CU first; at each level the LDS deep stack when
-    // it fits beside chunks of MIN_CAP, else the global one
-    for (int t = by_waves; t >= 1; --t) {
-      const size_t budget = LDS_CAP / t;
-      if (c->deep_pref != 2) {
-        ndl = c->ndeep;
-        cap = cap_for(budget);
-        if (fits(cap, budget) || (c->deep_pref == 1 && t == 1)) break;
-      }
-      if (c->deep_pref != 1) {
-        ndl = 0;
-        cap = cap_for(budget);
-        if (fits(cap, budget)) break;
-      }
-    }
+    // most workgroups per CU first
+    for (int t = by_waves; t >= 1; --t)
+      if (place(LDS_CAP / t, t == 1)) break;
   }
   const size_t lds = lds_bytes(c->S, c->C, c->R, cap, K, ndl);
   if (lds > LDS_CAP) return fail(PHY_EINVAL, "tree too large for LDS (tips of one block)");
@@ -1404,7 +1434,8 @@ int plan_chunks(phy_ctx* c) {
   HIP_TRY(hipMemcpy(c->d_prog, c->prog.data(), c->prog.size() * sizeof(int), hipMemcpyHostToDevice));
   c->cap_m = cap;
   c->nchunks = ch + 1;
-  c->deep_lds = ndl > 0;
+  c->deep_lds = ndl > 0 && ndl == c->ndeep;
+  c->ndl = ndl;
   return PHY_OK;
 }
 
@@ -1423,13 +1454,13 @@ int launch(phy_ctx* ctx, int n, const double* d_blens, const double* d_model, do
   const int budget = ctx->wg_budget > 0 ? ctx->wg_budget : ctx->wg_resident;
   const int gx = std::max(1, std::min(ctx->nblk, (budget + n - 1) / n));
   if ((size_t)gx * n > (size_t)ctx->wg_cap) return fail(PHY_ERANGE, "workgroup cap exceeded");
-  const size_t lds = lds_bytes(ctx->S, C, ctx->R, ctx->cap_m, ctx->K, ctx->deep_lds ? ctx->ndeep : 0);
+  const size_t lds = lds_bytes(ctx->S, C, ctx->R, ctx->cap_m, ctx->K, ctx->ndl);
   const int g_direct = (gx == 1) ? 1 : 0;
   SweepArgs sa{ctx->d_tips,  ctx->d_w,     ctx->d_pmat,  d_model,      ctx->d_scratch, ctx->d_dstk,
                ctx->d_gslot, ctx->d_sslot, d_site,       d_out,        ctx->d_mat_branch, ctx->d_eig,
                ctx->d_inner, ctx->S,       ctx->P,       ctx->Ppad,    C,              ctx->nsteps,
-               ctx->nslots,  ctx->ndeep,   ctx->nblk,    ctx->nmat,    ctx->R,         ctx->cap_m,
-               B,            phy_output_len(ctx), g_direct};
+               ctx->nslots,  ctx->ndeep,   ctx->ndl,     ctx->nblk,    ctx->nmat,    ctx->R,         ctx->cap_m,
+               B,            phy_output_len(ctx), g_direct, ctx->extra};
   hipEvent_t e0 = nullptr, e1 = nullptr;
   if (ctx->timing) {
     if (ctx->ev_used + 2 > (int)ctx->ev.size()) {
@@ -1587,7 +1618,7 @@ int phy_create(int S, int P, int C, int rooted, int model, const uint8_t* tipcod
   } while (0)
   HIP_C(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
   const size_t ncolwg = (size_t)C * WAVE;
-  TRY_C(dalloc(&c->d_tips, (size_t)S * c->Ppad));
+  TRY_C(dalloc(&c->d_tips, (size_t)S * c->Ppad / 2));
   TRY_C(dalloc(&c->d_w, (size_t)c->Ppad));
   TRY_C(dalloc(&c->d_prog, c->prog.size()));
   TRY_C(dalloc(&c->d_mat_branch, (size_t)c->nmat));
@@ -1604,12 +1635,16 @@ int phy_create(int S, int P, int C, int rooted, int model, const uint8_t* tipcod
   TRY_C(dalloc(&c->d_gslot, (size_t)c->wg_cap * C * c->nmat * 16));
   TRY_C(dalloc(&c->d_sslot, (size_t)c->wg_cap * C * 8));
   {
-    // tip bytes: (mask << 4) | record vector of the mask; padding = mask 15
-    std::vector<uint8_t> tips((size_t)S * c->Ppad, (uint8_t)((15 << 4) | vec_of[15]));
+    // tip nibbles: record vector of the pattern's mask (R <= 16); padding =
+    // mask 15; pattern 2j in the low nibble of byte j, 2j+1 in the high one
+    const int row = c->Ppad / 2;
+    const uint8_t pad = (uint8_t)vec_of[15];
+    std::vector<uint8_t> tips((size_t)S * row, (uint8_t)(pad | (pad << 4)));
     for (int t = 0; t < S; ++t)
       for (int i = 0; i < P; ++i) {
-        const int m = tipcodes[(size_t)t * P + i];
-        tips[(size_t)t * c->Ppad + i] = (uint8_t)((m << 4) | vec_of[m]);
+        const uint8_t v = (uint8_t)vec_of[tipcodes[(size_t)t * P + i]];
+        uint8_t& b = tips[(size_t)t * row + i / 2];
+        b = (i & 1) ? (uint8_t)((b & 0x0F) | (v << 4)) : (uint8_t)((b & 0xF0) | v);
       }
     std::vector<double> w(c->Ppad, 0.0);
     std::memcpy(w.data(), weights, sizeof(double) * P);
@@ -1759,14 +1794,14 @@ int phy_set_deep_stack(phy_ctx* ctx, int mode) {
   HIP_TRY(hipSetDevice(ctx->device));
   return plan_chunks(ctx);
 }
-int phy_deep_stack_in_lds(const phy_ctx* ctx) { return ctx ? (ctx->deep_lds ? 1 : 0) : -1; }
+int phy_deep_stack_in_lds(const phy_ctx* ctx) { return ctx ? ctx->ndl : -1; }
 
 int phy_lds_plan(const phy_ctx* ctx, int* n_chunks, int* matrices_per_chunk, int* lds_bytes_out) {
   if (!ctx) return fail(PHY_EINVAL, "NULL ctx");
   if (n_chunks) *n_chunks = ctx->nchunks;  // matrix-record chunks per pass
   if (matrices_per_chunk) *matrices_per_chunk = ctx->cap_m;
   if (lds_bytes_out)
-    *lds_bytes_out = (int)lds_bytes(ctx->S, ctx->C, ctx->R, ctx->cap_m, ctx->K, ctx->deep_lds ? ctx->ndeep : 0);
+    *lds_bytes_out = (int)lds_bytes(ctx->S, ctx->C, ctx->R, ctx->cap_m, ctx->K, ctx->ndl);
   return PHY_OK;
 }
 

@@ -170,7 +170,7 @@ class TreeLikelihood:
         _lib.check(self.lib.phy_lds_plan(self.ctx, *[ctypes.byref(v) for v in vals]), "phy_lds_plan")
         out = dict(zip(("n_chunks", "matrices_per_chunk", "lds_bytes"), [v.value for v in vals]))
         out["cols"] = self.lib.phy_columns_per_lane(self.ctx)
-        out["deep_lds"] = self.lib.phy_deep_stack_in_lds(self.ctx)
+        out["deep_lds_entries"] = self.lib.phy_deep_stack_in_lds(self.ctx)
         return out
 
     def timing_start(self):

@@ -113,7 +113,22 @@ def test_deep_stack_placement(mode, cols, seed, S, P, C, model, rooted, cat, wg)
     eng = _engine(case)
     eng.set_tuning(wg, cols, 0)
     eng.set_deep_stack(mode)
-    assert eng.lds_plan()["deep_lds"] == (1 if mode == 1 else 0)
+    depth = eng.program_info()["depth"]
+    assert eng.lds_plan()["deep_lds_entries"] == (depth if mode == 1 else 0)
+    check_case(case, eng)
+
+
+@pytest.mark.parametrize("lds_budget", [60000, 80000, 100000])
+def test_deep_stack_split(lds_budget):
+    """Automatic plan under tight LDS: the outer deep entries in LDS, the
+    inner ones in global memory (x operands read back from scratch slots)."""
+    case = cases.random_case(44, S=128, P=300, C=4, model="GTR")
+    eng = _engine(case)
+    eng.set_tuning(0, 2, lds_budget)
+    plan = eng.lds_plan()
+    depth = eng.program_info()["depth"]
+    assert 0 <= plan["deep_lds_entries"] <= depth
+    print("budget", lds_budget, "depth", depth, plan)
     check_case(case, eng)
 
 
