@@ -266,6 +266,18 @@ __device__ __forceinline__ V4 ld_v4(__amdgpu_buffer_rsrc_t srd, uint32_t off, ui
   return r;
 }
 
+// One 4-vector stored as two 16-B halves `half` bytes apart (dropped by the
+// buffer range check when `off` is out of range).
+__device__ __forceinline__ void st_v4(__amdgpu_buffer_rsrc_t srd, uint32_t off, uint32_t half, const V4& v) {
+  typedef unsigned u4 __attribute__((ext_vector_type(4)));
+  const u4 lo = {(unsigned)__double2loint(v.x), (unsigned)__double2hiint(v.x), (unsigned)__double2loint(v.y),
+                 (unsigned)__double2hiint(v.y)};
+  const u4 hi = {(unsigned)__double2loint(v.z), (unsigned)__double2hiint(v.z), (unsigned)__double2loint(v.w),
+                 (unsigned)__double2hiint(v.w)};
+  __builtin_amdgcn_raw_buffer_store_b128(lo, srd, off, 0, 0);
+  __builtin_amdgcn_raw_buffer_store_b128(hi, srd, off + half, 0, 0);
+}
+
 // s_waitcnt vmcnt(0) that the compiler's waitcnt pass sees (an inline-asm
 // wait would be invisible to it): clears loads left pending by staging
 // loops so the step loops are not charged a loop-carried vmcnt(0).
@@ -371,6 +383,14 @@ __global__ void __launch_bounds__(MAXT) __attribute__((amdgpu_waves_per_eu(K == 
   auto eoff = [&](int e, int k) __attribute__((always_inline)) -> uint32_t {  // byte offset of (entry, column k), half 0
     return (uint32_t)((((size_t)e * K + k) * 2 * ncolwg + colw) * 16);
   };
+  // Scratch offsets of this lane's live columns only: padding columns
+  // (pattern >= P) neither store nor load moved partials -- the range check
+  // drops their stores and zero-fills their loads, so they stay finite and
+  // their weight-0 upper partials are exactly zero.
+  unsigned vbits = 0;  // bit k: column k of the current block is a pattern
+  auto soff = [&](int e, int k) __attribute__((always_inline)) -> uint32_t {
+    return ((vbits >> k) & 1u) ? eoff(e, k) : scr_bytes;
+  };
   auto put = [&](double2* base, int e, int k, const V4& v) __attribute__((always_inline)) {
     double2* d = base + ((size_t)e * K + k) * 2 * ncolwg + colw;
     d[0] = make_double2(v.x, v.y);
@@ -468,6 +488,9 @@ __global__ void __launch_bounds__(MAXT) __attribute__((amdgpu_waves_per_eu(K == 
   };
 
   for (int blk = blockIdx.x; blk < a.nblk; blk += gridDim.x) {
+    vbits = 0;
+#pragma unroll
+    for (int k = 0; k < K; ++k) vbits |= (blk * WAVE * K + k * WAVE + lane < a.P) ? (1u << k) : 0u;
     __syncthreads();  // the previous block's tip / root-exchange reads are done
     // stage this block's tip bytes in LDS: S rows x 64K bytes, shared by the
     // C category-waves and by both passes (8 loads in flight per thread)
@@ -513,7 +536,7 @@ __global__ void __launch_bounds__(MAXT) __attribute__((amdgpu_waves_per_eu(K == 
         const bool need = more && (sn[ST_FLAGS] & F_XDEEP) && sn[ST_XDPOS] >= ndl;                                    \
         if (!DL)                                                                                                      \
       _Pragma("unroll")                                                                                               \
-        for (int k = 0; k < K; ++k) dnext[k] = ld_v4(srd_scr, need ? eoff(sn[ST_XSLOT], k) : scr_bytes, half_bytes);  \
+        for (int k = 0; k < K; ++k) dnext[k] = ld_v4(srd_scr, need ? soff(sn[ST_XSLOT], k) : scr_bytes, half_bytes);  \
       }                                                                                                               \
       ensure_chunk(st);                                                                                               \
       const int x = st[ST_X], y = st[ST_Y], fl = st[ST_FLAGS], vs = st[ST_VSLOT];                                     \
@@ -556,7 +579,7 @@ __global__ void __launch_bounds__(MAXT) __attribute__((amdgpu_waves_per_eu(K == 
           for (int k = 0; k < K; ++k) av[k] = pv[k];                                                                  \
         }                                                                                                             \
       _Pragma("unroll")                                                                                               \
-        for (int k = 0; k < K; ++k) if (!(PHY_ABLATE & 8)) put(scr, vs, k, av[k]);                                    \
+        for (int k = 0; k < K; ++k) if (!(PHY_ABLATE & 8)) st_v4(srd_scr, soff(vs, k), half_bytes, av[k]);                                    \
         if (fl & F_VDEEP) {                                                                                           \
           const int dp = st[ST_VDPOS];                                                                                \
           if (DL || dp < ndl)  /* a global entry is x's scratch slot itself */                                        \
@@ -600,13 +623,14 @@ __global__ void __launch_bounds__(MAXT) __attribute__((amdgpu_waves_per_eu(K == 
 #pragma unroll
     for (int k = 0; k < K; ++k) {
       const int i = blk * WAVE * K + k * WAVE + lane;  // pattern of this column
+      const bool live = i < a.P;  // padding columns contribute exactly nothing
       const double w = a.weights[i];
-      const double lnL = log(L[k]);
+      const double lnL = live ? log(L[k]) : 0.0;
       if (c == 0) {
         acc_ll += w * lnL;
-        if (a.site_ll != nullptr && i < a.P) a.site_ll[(size_t)draw * a.P + i] = lnL;
+        if (a.site_ll != nullptr && live) a.site_ll[(size_t)draw * a.P + i] = lnL;
       }
-      const double sc = w / L[k];
+      const double sc = live ? w / L[k] : 0.0;
       const double s_c = sc * ps_c;
       acc_dps = fma(sc, fp[k], acc_dps);
       acc_f.x = fma(s_c, proot[k].x, acc_f.x);
@@ -636,8 +660,8 @@ __global__ void __launch_bounds__(MAXT) __attribute__((amdgpu_waves_per_eu(K == 
       const int xs = sp[ST_XSLOT], ys = sp[ST_YSLOT], vd = sp[ST_VDPOS];         \
       _Pragma("unroll")                                                          \
       for (int k = 0; k < K; ++k) {                                              \
-        r.lx[k] = ld_v4(srd_scr, lx ? eoff(xs, k) : scr_bytes, half_bytes);      \
-        r.ly[k] = ld_v4(srd_scr, ly ? eoff(ys, k) : scr_bytes, half_bytes);      \
+        r.lx[k] = ld_v4(srd_scr, lx ? soff(xs, k) : scr_bytes, half_bytes);      \
+        r.ly[k] = ld_v4(srd_scr, ly ? soff(ys, k) : scr_bytes, half_bytes);      \
         if constexpr (!DL)                                                       \
           r.lr[k] = ld_v4(srd_dsk, lr ? eoff(vd, k) : dsk_bytes, half_bytes);    \
       }                                                                          \
