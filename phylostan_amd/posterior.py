@@ -7,7 +7,8 @@ the transformed parameters (site rates, node heights, branch lengths), the
 priors and the log-Jacobian of the height reparametrisation.  Its gradient is
 assembled by hand (reverse mode) around the engine's outputs:
 
-  dlogL/dblens   -> rate, node heights -> props, root height
+  dlogL/dblens   -> rate (strict) or per-branch substrates (relaxed clocks),
+                    node heights -> props, root height
   dlogL/drs, /dps-> Weibull shape (+ pinv), or the discrete-rate simplices
   dlogL/dP[c][b] -> kappa / GTR exchangeabilities and frequencies through the
                     eigendecomposition (``models.q_param_gradients``)
@@ -18,16 +19,18 @@ columns a Stan sample CSV would hold.
 
 Supported ``build`` options (``phylostan/phylostan.py:69-95``): models JC69 /
 HKY / GTR; ``-C`` Weibull categories (+ ``--invariant``) or ``--heterogeneity
-discrete``; no clock (unrooted, ``blens ~ exponential(10)``) or ``--clock
-strict`` with ``--estimate_rate`` or a fixed ``--rate``; ``--coalescent``
-constant / skyride / skygrid; ``--heterochronous``.  The relaxed clocks and
-the birth-death prior are out of scope and are refused
-loudly.
+discrete``; no clock (unrooted, ``blens ~ exponential(10)``), ``--clock
+strict`` with ``--estimate_rate`` or a fixed ``--rate``, or a relaxed clock
+(``ucln``, ``uced``, ``ace``, ``acln``, ``acg``, ``aoup``, ``gmrf``,
+``hsmrf``; ``clocks.py``); ``--coalescent`` constant / skyride / skygrid;
+``--speciation bd`` (``yule`` adds nothing, as emitted); ``--heterochronous``.
+Phylogeography (``--geo``) is refused loudly.
 """
 import math
 
 import numpy as np
 
+from . import clocks
 from . import models
 from . import priors
 from .transforms import Identity, Lower, Simplex, Unit
@@ -41,10 +44,16 @@ class ModelSpec:
                  rate=None, lower_root=0.0, grid=None, cutoff=None, speciation=None):
         if model not in models.MODEL_IDS:
             raise ValueError("model must be JC69, HKY or GTR")
-        if clock not in (None, "strict"):
-            raise NotImplementedError("clock %r is not supported (strict or none)" % clock)
-        if speciation is not None:
-            raise NotImplementedError("speciation priors are not supported")
+        if clock not in (None, "strict") + clocks.RELAXED:
+            raise ValueError("unknown clock %r" % clock)
+        if clock in clocks.AUTOCORR and not estimate_rate:
+            # heights_to_blens_autocorr reads substrates, which only exist
+            # with --estimate_rate: the emitted model would not compile
+            raise ValueError("clock %r needs --estimate_rate" % clock)
+        if speciation not in (None, "bd", "yule"):
+            raise ValueError("unknown speciation model %r" % speciation)
+        if speciation is not None and clock is None:
+            raise ValueError("a speciation prior needs a clock")
         if coalescent not in (None, "constant", "skyride", "skygrid"):
             raise ValueError("unknown coalescent %r" % coalescent)
         if clock is None and coalescent is not None:
@@ -65,6 +74,13 @@ class ModelSpec:
         self.lower_root = float(lower_root)
         self.grid = grid
         self.cutoff = cutoff
+        self.speciation = speciation
+
+    @property
+    def relaxed(self):
+        """A relaxed clock with per-branch substrates (needs --estimate_rate;
+        without it ucln/uced fall back to the strict blens, as emitted)."""
+        return self.clock in clocks.RELAXED and self.estimate_rate
 
     @property
     def C(self):
@@ -153,7 +169,26 @@ class Posterior:
         if self.clock:
             P.append(_Param("props", Unit(self.S - 2)))
             if sp.estimate_rate:
-                P.append(_Param("rate", Lower(0.0)))
+                if sp.clock == "strict":
+                    P.append(_Param("rate", Lower(0.0)))
+                elif sp.clock in clocks.MRF:
+                    P.append(_Param("deltas", Identity(2 * self.S - 3)))
+                    P.append(_Param("rate", Lower(0.0)))
+                    P.append(_Param("zeta", Lower(0.0)))
+                    if sp.clock == "hsmrf":
+                        P.append(_Param("gammas", Lower(0.0, self.B - 1)))
+                else:
+                    P.append(_Param("substrates", Lower(0.0, self.B)))
+                    if sp.clock in ("acln", "acg"):
+                        P.append(_Param("nu", Lower(0.0)))
+                    elif sp.clock == "aoup":
+                        P.append(_Param("beta", Lower(0.0)))
+                        P.append(_Param("sigma", Lower(0.0)))
+                    elif sp.clock == "ucln":
+                        P.append(_Param("ucln_mean", Lower(0.0)))
+                        P.append(_Param("ucln_stdev", Lower(0.0)))
+                    elif sp.clock == "uced":
+                        P.append(_Param("uced_mean", Lower(0.0)))
             P.append(_Param("height", Lower(self.lower_root)))
             if sp.coalescent == "constant":
                 P.append(_Param("theta", Lower(0.0)))
@@ -163,6 +198,9 @@ class Posterior:
             elif sp.coalescent == "skygrid":
                 P.append(_Param("thetas", Identity(int(sp.grid) - 1)))
                 P.append(_Param("tau", Lower(0.0)))
+            if sp.speciation == "bd":
+                P.append(_Param("netDiversificationRate", Lower(0.0)))
+                P.append(_Param("relativeExtinctionRate", Unit()))
         else:
             P.append(_Param("blens", Lower(0.0, self.B)))
         if sp.model == "GTR":
@@ -232,6 +270,7 @@ class Posterior:
         self.b_lower = self.lowers[bnodes]
         self.times_internal = np.zeros(2 * S - 1, bool)
         self.times_internal[S:] = True
+        self.ctree = clocks.ClockTree(S, t.map1) if self.spec.relaxed else None
 
     def _dropped_constants(self):
         """Normalising constants Stan's ``~`` statements drop (propto) -- added
@@ -241,8 +280,10 @@ class Posterior:
         if sp.categories > 1 and sp.heterogeneity == "weibull":
             c += math.log(1.0)  # wshape ~ exponential(1)
         if self.clock:
-            if sp.estimate_rate:
+            if sp.estimate_rate and sp.clock == "strict":
                 c += math.log(1000.0)
+            if sp.relaxed:
+                c += clocks.dropped_constants(sp.clock, self.B, 2 * self.S - 3)
             if sp.coalescent in ("skyride", "skygrid"):
                 a = b = 0.001
                 c += -math.lgamma(a) + a * math.log(b)
@@ -305,10 +346,24 @@ class Posterior:
             h[:, nodes - S] = low + (h[:, pidx] - low) * props[:, jidx]
         return h
 
-    def _blens_from_heights(self, h, rate):
+    def _span(self, h):
+        """Branch durations [n, B]: heights[parent] - heights[node] (tips: - lowers)."""
         base = np.where(self.b_internal, h[:, self.b_hidx], self.b_lower)
-        span = h[:, self.b_parent] - base
-        return rate[:, None] * span, span
+        return h[:, self.b_parent] - base
+
+    def _substrates(self, vals):
+        """Per-branch substrates of a relaxed clock [n, B] (MRF: transformed
+        from deltas and rate, get_rates_from_deltas)."""
+        if self.spec.clock in clocks.MRF:
+            return clocks.rates_from_deltas(self.ctree, vals["deltas"], vals["rate"])
+        return vals["substrates"]
+
+    def _multiplier(self, vals, n):
+        """blens = span * mult: (mult [n, B], substrates or None)."""
+        if self.spec.relaxed:
+            r = self._substrates(vals)
+            return clocks.blens_multiplier(self.ctree, self.spec.clock, r), r
+        return np.repeat(self._rate(vals, n)[:, None], self.B, axis=1), None
 
     def _rate(self, vals, n):
         if self.spec.estimate_rate:
@@ -345,6 +400,8 @@ class Posterior:
             out += [("ps", ps), ("rs", rs)]
         if self.clock:
             out.append(("heights", self._heights(vals, n)))
+            if sp.relaxed and sp.clock in clocks.MRF:
+                out.append(("substrates", self._substrates(vals)))
         return out
 
     def blens(self, U):
@@ -354,7 +411,7 @@ class Posterior:
         vals, _, _ = self.constrain(U)
         if not self.clock:
             return vals["blens"]
-        return self._blens_from_heights(self._heights(vals, n), self._rate(vals, n))[0]
+        return self._span(self._heights(vals, n)) * self._multiplier(vals, n)[0]
 
     # ------------------------------------------------------- value + gradient
     def log_prob_grad(self, U, propto=True, need_grad=True):
@@ -373,9 +430,10 @@ class Posterior:
 
         # ---- branch lengths
         if self.clock:
-            rate = self._rate(vals, n)
             h = self._heights(vals, n)
-            blens, span = self._blens_from_heights(h, rate)
+            span = self._span(h)
+            mult, subs = self._multiplier(vals, n)
+            blens = span * mult
         else:
             blens = vals["blens"]
 
@@ -407,9 +465,22 @@ class Posterior:
         g_h = None
         if self.clock:
             g_h = np.zeros((n, S - 1))
-            if sp.estimate_rate:
+            g_subs_prior = g_span_prior = None
+            if sp.estimate_rate and sp.clock == "strict":
                 lp = lp - 1000.0 * vals["rate"]
                 gx["rate"] -= 1000.0
+            elif sp.relaxed:
+                c_lp, g_subs_prior, g_span_prior, gh = clocks.clock_prior(self.ctree, sp.clock, vals, subs, span)
+                lp = lp + c_lp
+                for name, g in gh.items():
+                    gx[name] += g
+            if sp.speciation == "bd":
+                b_lp, g_hb, g_a, g_r = clocks.birth_death(h, vals["netDiversificationRate"],
+                                                          vals["relativeExtinctionRate"])
+                lp = lp + b_lp
+                g_h += g_hb
+                gx["netDiversificationRate"] += g_a
+                gx["relativeExtinctionRate"] += g_r
             # log-Jacobian of the height transform (generate_script.py:739-752)
             nr = self.nonroot_int
             gap = h[:, self.parent[nr] - S] - self.lowers[nr]
@@ -465,9 +536,19 @@ class Posterior:
                     gx["kappa"][d] += models.kappa_gradient(gr)
         self._site_rates_backward(vals, g_rs, g_ps, gx, rs, ps)
         if self.clock:
-            gspan = g_bl * rate[:, None]
-            if sp.estimate_rate:
-                gx["rate"] += (g_bl * span).sum(axis=1)
+            gspan = g_bl * mult
+            g_mult = g_bl * span
+            if sp.relaxed:
+                gspan = gspan + g_span_prior
+                g_subs = clocks.blens_multiplier_backward(self.ctree, sp.clock, g_mult) + g_subs_prior
+                if sp.clock in clocks.MRF:
+                    g_d, g_rate = clocks.rates_from_deltas_backward(self.ctree, subs, g_subs)
+                    gx["deltas"] += g_d
+                    gx["rate"] += g_rate
+                else:
+                    gx["substrates"] += g_subs
+            elif sp.estimate_rate:
+                gx["rate"] += g_mult.sum(axis=1)
             np.add.at(g_h.T, self.b_parent, gspan.T)
             np.add.at(g_h.T, self.b_hidx[self.b_internal], -gspan[:, self.b_internal].T)
             # heights <- props, height (reverse of the level sweep)

@@ -75,9 +75,28 @@ def test_run_nuts_two_chains_and_parse(tmp_path, capsys):
     assert open(str(tmp_path / "p.trees")).read().count("tree ") == 20
 
 
+def test_run_relaxed_clock_vb(tmp_path, capsys):
+    """--clock ucln --estimate_rate: substrates in the sample CSV, per-branch
+    rates in the trees file (utils.py:229-245)."""
+    t, a = fixture_files.write_random_dataset(str(tmp_path), seed=3, S=6, sites=50)
+    out = str(tmp_path / "ucln")
+    post, lines = _run(["-s", str(tmp_path / "x.stan"), "-m", "JC69", "--clock", "ucln", "--estimate_rate",
+                        "--coalescent", "constant", "--heterochronous", "-t", t, "-i", a,
+                        "-o", out, "-S", "5", "--iter", "200", "--elbo_samples", "10", "--samples", "20",
+                        "--tol_rel_obj", "0.01"])
+    header, data = stan_io.read_samples(out)
+    assert "substrates.10" in header and "ucln_stdev" in header
+    assert data.shape == (21, len(header))
+    trees = open(out + ".trees").read()
+    assert trees.count("tree ") == 21 and ",rate=" in trees
+    capsys.readouterr()
+
+
 def test_unsupported_options_fail_loudly(tmp_path):
     t, a = fixture_files.write_random_dataset(str(tmp_path), seed=1, S=5, sites=20)
-    with pytest.raises((SystemExit, NotImplementedError)):
-        _run(["-s", "x", "-t", t, "-i", a, "-o", str(tmp_path / "o"), "--clock", "ucln"])
+    with pytest.raises((SystemExit, ValueError)):
+        _run(["-s", "x", "-t", t, "-i", a, "-o", str(tmp_path / "o"), "--clock", "acln"])  # needs --estimate_rate
+    with pytest.raises(SystemExit):
+        _run(["-s", "x", "-t", t, "-i", a, "-o", str(tmp_path / "o"), "--geo"])
     with pytest.raises(SystemExit):
         _run(["-s", "x", "-t", t, "-i", a, "-o", str(tmp_path / "o"), "-a", "hmc"])

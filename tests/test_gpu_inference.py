@@ -25,14 +25,14 @@ README_CI = {  # README.md:104-108 (fluA meanfield ADVI)
 }
 
 
-def _fluA_posterior(lik_cls, **kw):
+def _fluA_posterior(lik_cls, clock="strict", speciation=None, **kw):
     from phylostan_amd.posterior import ModelSpec, Posterior, TreeData
     d = cases.load_layout("fluA")
     S = d["tipbits"].shape[0]
     peel0 = d["peel"] - 1
     tree = TreeData(S, peel0, d["map"], d["lowers"], float(d["oldest"]))
-    spec = ModelSpec(model="HKY", categories=4, clock="strict", estimate_rate=True, coalescent="constant",
-                     heterochronous=True)
+    spec = ModelSpec(model="HKY", categories=4, clock=clock, estimate_rate=True, coalescent="constant",
+                     heterochronous=True, speciation=speciation)
     return Posterior(spec, tree, lik_cls(d["tipbits"], d["weights"], peel0, True, "HKY", 4, **kw)), d
 
 
@@ -47,6 +47,31 @@ def test_posterior_gpu_equals_oracle():
     U = np.stack([u0] + [u0 + 0.05 * rng.standard_normal(pg.dim) for _ in range(3)])
     lg, Gg = pg.log_prob_grad(U)
     lo, Go = po.log_prob_grad(U)
+    np.testing.assert_allclose(lg, lo, rtol=1e-10)
+    for k in range(len(U)):
+        assert np.max(np.abs(Gg[k] - Go[k])) <= 1e-8 * np.max(np.abs(Go[k]))
+
+
+@pytest.mark.parametrize("clock,speciation", [("ucln", None), ("acln", None), ("hsmrf", "bd")])
+def test_relaxed_clock_posterior_gpu_equals_oracle(clock, speciation):
+    """Relaxed clocks (per-branch substrates in the blens) and the
+    birth-death prior around the GPU likelihood: value and gradient equal
+    the oracle-backed posterior's."""
+    from phylostan_amd.engine import TreeLikelihood
+    pg, d = _fluA_posterior(TreeLikelihood, clock=clock, speciation=speciation, max_draws=4)
+    po, _ = _fluA_posterior(OracleLikelihood, clock=clock, speciation=speciation)
+    rng = np.random.default_rng(1)
+    case = cases.fluA_case()
+    vals = dict(wshape=0.488, height=d["heights"][-1], theta=4.03, kappa=5.58, freqs=case.freqs,
+                props=pg.props_from_heights(d["heights"]), substrates=rng.uniform(0.004, 0.006, pg.B),
+                ucln_mean=0.005, ucln_stdev=0.3, nu=0.01, deltas=rng.normal(0, 0.001, 2 * pg.S - 3),
+                rate=0.005, zeta=1.0, gammas=np.ones(pg.B - 1), netDiversificationRate=0.1,
+                relativeExtinctionRate=0.5)
+    u0 = pg.unconstrain({p.name: vals[p.name] for p in pg.params})
+    U = np.stack([u0] + [u0 + 0.02 * rng.standard_normal(pg.dim) for _ in range(3)])
+    lg, Gg = pg.log_prob_grad(U)
+    lo, Go = po.log_prob_grad(U)
+    assert np.all(np.isfinite(lg))
     np.testing.assert_allclose(lg, lo, rtol=1e-10)
     for k in range(len(U)):
         assert np.max(np.abs(Gg[k] - Go[k])) <= 1e-8 * np.max(np.abs(Go[k]))

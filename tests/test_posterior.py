@@ -209,7 +209,7 @@ def test_skygrid_and_gmrf_gradients():
 
 # ------------------------------------------------------- whole posterior
 def _random_posterior(seed, model, C, clock, coalescent=None, invariant=False, hetero=False,
-                      heterogeneity="weibull", S=7, P=40):
+                      heterogeneity="weibull", S=7, P=40, speciation=None):
     case = cases.random_case(seed, S=S, P=P, C=1, model=model, rooted=clock is not None)
     rng = np.random.default_rng(seed)
     tips = rng.uniform(0, 1.0, S) if hetero else np.zeros(S)
@@ -217,7 +217,8 @@ def _random_posterior(seed, model, C, clock, coalescent=None, invariant=False, h
                     float(tips.max()) if hetero else None)
     spec = ModelSpec(model=model, categories=C, invariant=invariant, heterogeneity=heterogeneity, clock=clock,
                      estimate_rate=clock is not None, coalescent=coalescent, heterochronous=hetero,
-                     grid=5 if coalescent == "skygrid" else None, cutoff=2.0 if coalescent == "skygrid" else None)
+                     grid=5 if coalescent == "skygrid" else None, cutoff=2.0 if coalescent == "skygrid" else None,
+                     speciation=speciation)
     lik = OracleLikelihood(case.tipcodes, case.weights, case.peel0, clock is not None, model, spec.C)
     return Posterior(spec, tree, lik), rng
 
@@ -230,7 +231,34 @@ CONFIGS = [
     dict(model="GTR", C=3, clock="strict", coalescent="skyride"),
     dict(model="GTR", C=3, clock="strict", coalescent="skygrid", hetero=True, invariant=True),
     dict(model="JC69", C=3, clock="strict", coalescent=None, heterogeneity="discrete"),
+    dict(model="HKY", C=1, clock="ucln", coalescent="constant"),
+    dict(model="JC69", C=2, clock="uced", coalescent="skyride", hetero=True),
+    dict(model="GTR", C=1, clock="ace", coalescent="constant", hetero=True),
+    dict(model="HKY", C=3, clock="acln", coalescent="constant", hetero=True),
+    dict(model="JC69", C=1, clock="acg", coalescent="constant"),
+    dict(model="JC69", C=1, clock="aoup", coalescent="constant", hetero=True),
+    dict(model="HKY", C=1, clock="gmrf", coalescent="constant"),
+    dict(model="GTR", C=2, clock="hsmrf", coalescent="skyride", hetero=True),
+    dict(model="HKY", C=1, clock="strict", coalescent="constant", speciation="bd"),
+    dict(model="JC69", C=1, clock="ucln", coalescent=None, speciation="bd", hetero=True),
 ]
+
+
+def _relaxed_start(post, rng, u):
+    """Start a relaxed-clock chain where its priors are finite and moderate."""
+    for name, val in (("rate", 0.3), ("ucln_mean", 0.3), ("uced_mean", 0.3), ("nu", 0.5), ("beta", 0.7),
+                      ("sigma", 0.2), ("zeta", 50.0), ("netDiversificationRate", 0.4),
+                      ("relativeExtinctionRate", 0.6), ("ucln_stdev", 0.5)):
+        p = post.param(name)
+        if p is not None:
+            u[p.sl] = p.tr.unconstrain(np.array([val]))[0]
+    p = post.param("substrates")
+    if p is not None:
+        u[p.sl] = np.log(rng.uniform(0.2, 0.4, p.tr.size))
+    p = post.param("deltas")
+    if p is not None:
+        u[p.sl] = rng.normal(0.0, 0.05, p.tr.size)
+    return u
 
 
 @pytest.mark.parametrize("cfg", CONFIGS, ids=lambda c: "-".join(str(v) for v in c.values()))
@@ -239,6 +267,7 @@ def test_posterior_gradient_fd(cfg):
     u = rng.uniform(-1.0, 1.0, post.dim)
     if post.param("rate") is not None:
         u[post.param("rate").sl] = math.log(0.3)
+    u = _relaxed_start(post, rng, u)
     check_grad(post, u)
 
 
@@ -277,7 +306,143 @@ def test_batched_equals_single():
 
 
 def test_unsupported_options_are_loud():
-    with pytest.raises(NotImplementedError):
-        ModelSpec(model="GTR", clock="ucln")
+    with pytest.raises(ValueError):
+        ModelSpec(model="GTR", clock="acln")  # autocorrelated clocks need --estimate_rate
+    with pytest.raises(ValueError):
+        ModelSpec(model="GTR", speciation="bd")  # needs a clock
     with pytest.raises(ValueError):
         ModelSpec(model="GTR", categories=4, invariant=True, heterogeneity="discrete")
+
+
+# ------------------------------------------- relaxed clocks: Stan restatements
+def _stan_rows(map1):
+    return [(int(a), int(b)) for a, b in map1]
+
+
+def _pr(map1, i):
+    """Stan: the parent-rate node of row i (1-based): map[2,1] for the root's children."""
+    node_count = len(map1)
+    return map1[1][0] if map1[i - 1][1] == node_count else map1[i - 1][1]
+
+
+def _span1(map1, heights, lowers, S, i):
+    """heights[map[i,2]-S] - heights[map[i,1]-S]   (tips: - lowers[map[i,1]])."""
+    node, par = map1[i - 1]
+    low = heights[node - S - 1] if node > S else lowers[node - 1]
+    return heights[par - S - 1] - low
+
+
+def _lnorm(y, mu, sd):
+    return -math.log(y) - math.log(sd) - 0.5 * math.log(2 * math.pi) - (math.log(y) - mu) ** 2 / (2 * sd * sd)
+
+
+def _stan_clock(clock, map1, rates, heights, lowers, S, nu=None, beta=None, sig=None):
+    """Literal loops of ace_log / acln_log / acg_log / aoup_log
+    (generate_script.py:103-246), full lpdfs (constants kept)."""
+    node_count = len(map1)
+    lp = 0.0
+    for i in range(3, node_count + 1):
+        node = map1[i - 1][0]
+        ra = rates[_pr(map1, i) - 1]
+        y = rates[node - 1]
+        t = _span1(map1, heights, lowers, S, i)
+        if clock == "ace":
+            lp += math.log(1.0 / ra) - y / ra
+        elif clock == "acln":
+            lp += _lnorm(y, math.log(ra) - nu * t / 2.0, math.sqrt(nu * t))
+        elif clock == "acg":
+            a, b = ra * ra / (nu * t), ra / (nu * t)
+            lp += a * math.log(b) - math.lgamma(a) + (a - 1) * math.log(y) - b * y
+        elif clock == "aoup":
+            mean = (ra if map1[i - 1][1] == node_count else y) * math.exp(-beta * t)
+            sd = math.sqrt(sig * (1.0 - math.exp(-2.0 * beta * t)) / (2.0 * beta))
+            lp += -math.log(sd) - 0.5 * math.log(2 * math.pi) - (y - mean) ** 2 / (2 * sd * sd)
+    return lp
+
+
+def _stan_blens_autocorr(map1, subs, heights, lowers, S):
+    node_count = len(map1)
+    bl = np.zeros(2 * S - 2)
+    for j in range(2, node_count + 1):
+        bl[map1[j - 1][0] - 1] = _span1(map1, heights, lowers, S, j)
+    bl[map1[1][0] - 1] *= subs[map1[1][0] - 1]
+    for j in range(3, node_count + 1):
+        node = map1[j - 1][0]
+        bl[node - 1] *= 0.5 * (subs[node - 1] + subs[_pr(map1, j) - 1])
+    return bl
+
+
+def _stan_rates_from_deltas(map1, deltas, rate, S):
+    subs = np.zeros(2 * S - 2)
+    subs[map1[1][0] - 1] = rate
+    for i in range(3, len(map1) + 1):
+        subs[map1[i - 1][0] - 1] = math.exp(deltas[i - 3] + math.log(subs[_pr(map1, i) - 1]))
+    return subs
+
+
+def _stan_birth_death(heights, map1, rho, a, r, S):
+    node_count = S + len(heights)
+    lp = 0.0
+    for i in range(1, node_count + 1):
+        if map1[i - 1][0] > S:
+            mrh = -r * heights[map1[i - 1][0] - S - 1]
+            z = math.log(rho + ((1.0 - rho) - a) * math.exp(mrh))
+            lp += -2.0 * z + mrh
+            if map1[i - 1][0] == 1:
+                lp += mrh - z
+    return lp + (S - 1) * math.log(r * rho) + node_count * math.log(1.0 - a)
+
+
+@pytest.mark.parametrize("hetero", [False, True])
+def test_relaxed_clock_restatements(hetero):
+    from phylostan_amd import clocks
+    rng = np.random.default_rng(21 + hetero)
+    S = 9
+    peel = cases.random_peel(S, rng)
+    map1 = preorder_map(peel)
+    rows = _stan_rows(map1)
+    tips = rng.uniform(0, 1, S) if hetero else np.zeros(S)
+    low = lowers_for(peel, tips)
+    t = np.zeros(2 * S - 1)
+    t[:S] = tips
+    for a, b, v in peel:
+        t[v] = max(t[a], t[b]) + rng.exponential(0.4)
+    heights = t[S:]
+    ct = clocks.ClockTree(S, map1)
+    subs = rng.uniform(0.2, 0.6, 2 * S - 2)
+    # span as the posterior forms it
+    parent = np.zeros(2 * S - 1, int)
+    for a, b, v in peel:
+        parent[a] = parent[b] = v
+    span = (t[parent[:2 * S - 2]] - np.where(np.arange(2 * S - 2) >= S, t[:2 * S - 2], low[:2 * S - 2]))[None]
+    r = subs[None]
+    nterms = 2 * S - 3
+    l, *_ = clocks._ace(ct, r)
+    assert abs(l[0] - _stan_clock("ace", rows, subs, heights, low, S)) < 1e-10
+    l, *_ = clocks._acln(ct, r, span, np.array([0.7]))
+    assert abs(l[0] - nterms * clocks.HALF_LOG_2PI - _stan_clock("acln", rows, subs, heights, low, S, nu=0.7)) < 1e-10
+    l, *_ = clocks._acg(ct, r, span, np.array([0.7]))
+    assert abs(l[0] - _stan_clock("acg", rows, subs, heights, low, S, nu=0.7)) < 1e-9
+    l, *_ = clocks._aoup(ct, r, span, np.array([0.8]), np.array([0.3]))
+    assert abs(l[0] - nterms * clocks.HALF_LOG_2PI
+               - _stan_clock("aoup", rows, subs, heights, low, S, beta=0.8, sig=0.3)) < 1e-10
+    bl = span[0] * clocks.blens_multiplier(ct, "acln", r)[0]
+    np.testing.assert_allclose(bl, _stan_blens_autocorr(rows, subs, heights, low, S), rtol=1e-14)
+    deltas = rng.normal(0, 0.3, 2 * S - 3)
+    np.testing.assert_allclose(clocks.rates_from_deltas(ct, deltas[None], np.array([0.4]))[0],
+                               _stan_rates_from_deltas(rows, deltas, 0.4, S), rtol=1e-14)
+    lbd, *_ = clocks.birth_death(heights[None], np.array([0.3]), np.array([0.8]))
+    assert abs(lbd[0] - _stan_birth_death(heights, rows, 1.0, 0.3, 0.8, S)) < 1e-10
+
+
+def test_relaxed_clock_csv_columns():
+    post, _ = _random_posterior(5, model="HKY", C=1, clock="hsmrf", coalescent="constant")
+    names = post.column_names()
+    S = post.S
+    i = names.index
+    assert i("props.1") < i("deltas.1") < i("rate") < i("zeta") < i("gammas.1") < i("height") < i("theta")
+    assert i("heights.1") < i("substrates.1") and "substrates.%d" % (2 * S - 2) in names
+    post, _ = _random_posterior(5, model="JC69", C=1, clock="ucln", speciation="bd")
+    names = post.column_names()
+    assert names.index("substrates.1") < names.index("ucln_mean") < names.index("ucln_stdev") \
+        < names.index("height") < names.index("netDiversificationRate") < names.index("relativeExtinctionRate")
