@@ -80,6 +80,40 @@ enum {
 constexpr int F_MV = 1;     // the step's branch has a matrix (else identity)
 constexpr int F_XDEEP = 2;  // both children internal: x's operand is on the deep stack
 constexpr int F_VDEEP = 4;  // v is the x child of a both-internal parent
+
+// The device copy of the program packs a step into 8 ints (pack_program):
+//   w0 x | y<<16   w1 mx | my<<16   w2 mv | vslot<<16   w3 xslot | yslot<<16
+//   w4 flags | xdpos<<8 | vdpos<<16 (8-bit fields)      w5 chunk | m0<<16
+//   w6 mn | node<<16                                    w7 unused
+// 16-bit fields are signed (-1 = none).  One s_load_dwordx8 per step, issued
+// a step ahead, replaces a chain of dependent scalar loads.
+constexpr int PSTEP = 8;
+struct Step {
+  int x, y, mx, my, mv, vs, fl, xs, ys, xd, vd, ch, m0, mn;
+};
+__device__ __forceinline__ int lo16(int w) { return (int)(short)(w & 0xFFFF); }
+__device__ __forceinline__ int hi16(int w) { return w >> 16; }
+__device__ __forceinline__ int b8(int w, int k) { return (int)(signed char)((w >> (8 * k)) & 0xFF); }
+__device__ __forceinline__ Step ld_step(const int* __restrict__ prog, int s) {
+  const int4 a = *reinterpret_cast<const int4*>(prog + s * PSTEP);
+  const int4 b = *reinterpret_cast<const int4*>(prog + s * PSTEP + 4);
+  Step t;
+  t.x = lo16(a.x);
+  t.y = hi16(a.x);
+  t.mx = lo16(a.y);
+  t.my = hi16(a.y);
+  t.mv = lo16(a.z);
+  t.vs = hi16(a.z);
+  t.xs = lo16(a.w);
+  t.ys = hi16(a.w);
+  t.fl = b.x & 0xFF;
+  t.xd = b8(b.x, 1);
+  t.vd = b8(b.x, 2);
+  t.ch = lo16(b.y);
+  t.m0 = hi16(b.y);
+  t.mn = lo16(b.z);
+  return t;
+}
 // Per-draw eigensystem record: P(t) = m1 diag(exp(lam t)) m2, plus Q.
 constexpr int EIG_LEN = 56;  // m1[16] lam[4] m2[16] Q[16] (+pad)
 constexpr int EIG_M1 = 0, EIG_LAM = 16, EIG_M2 = 20, EIG_Q = 36;
@@ -424,10 +458,10 @@ __global__ void __launch_bounds__(MAXT) __attribute__((amdgpu_waves_per_eu(K == 
 
   // ---- this wave's chunk of matrix records in LDS (no barrier: private) ----
   int cur = -1, m0 = 0;
-  auto ensure_chunk = [&](const int* st) {
-    const int ch = st[ST_CHUNK];
+  auto ensure_chunk = [&](const Step& st) {
+    const int ch = st.ch;
     if (ch == cur) return;  // wave-uniform
-    const int lo = st[ST_M0], n = st[ST_MN];
+    const int lo = st.m0, n = st.mn;
     const double2* src = reinterpret_cast<const double2*>(pmat_c + (size_t)lo * rec);
     double2* dst = reinterpret_cast<double2*>(mats);
     const int q2 = n * rec / 2;
@@ -527,22 +561,21 @@ __global__ void __launch_bounds__(MAXT) __attribute__((amdgpu_waves_per_eu(K == 
     // dcur: this step's deep operand (loaded one step ahead into dnext,
     // alternating by name across an unrolled pair of steps: no register
     // copy of an in-flight load)
-    #define FSTEP(s, dcur, dnext) do {                                                                                \
-      const int* st = prog + s * STEP_INTS;                                                                           \
-      {                                                                                                               \
-        const bool more = s + 1 < nsteps;                                                                             \
-        const int* sn = prog + (more ? s + 1 : s) * STEP_INTS;                                                        \
-        /* an x operand whose deep entry is global is read back from x's scratch slot */                              \
-        const bool need = more && (sn[ST_FLAGS] & F_XDEEP) && sn[ST_XDPOS] >= ndl;                                    \
+    #define FSTEP(s, dcur, dnext, st, sn) do {                                            \
+      {                                                                                   \
+        const bool more = s + 1 < nsteps;                                                 \
+        sn = ld_step(prog, more ? s + 1 : s); /* next step's record, a step ahead */      \
+        /* an x operand whose deep entry is global is read back from x's scratch slot */  \
+        const bool need = more && (sn.fl & F_XDEEP) && sn.xd >= ndl;                      \
         if (!DL)                                                                                                      \
       _Pragma("unroll")                                                                                               \
-        for (int k = 0; k < K; ++k) dnext[k] = ld_v4(srd_scr, need ? soff(sn[ST_XSLOT], k) : scr_bytes, half_bytes);  \
+        for (int k = 0; k < K; ++k) dnext[k] = ld_v4(srd_scr, need ? soff(sn.xs, k) : scr_bytes, half_bytes);         \
       }                                                                                                               \
       ensure_chunk(st);                                                                                               \
-      const int x = st[ST_X], y = st[ST_Y], fl = st[ST_FLAGS], vs = st[ST_VSLOT];                                     \
+      const int x = st.x, y = st.y, fl = st.fl, vs = st.vs;                        \
       V4 ax[K], ay[K], pv[K];                                                                                         \
       if (y >= 0) {                                                                                                   \
-        const int my = st[ST_MY];                                                                                     \
+        const int my = st.my;                                                                                     \
       _Pragma("unroll")                                                                                               \
         for (int k = 0; k < K; ++k) ay[k] = look(my, tipb(y, k));                                                     \
       } else {                                                                                                        \
@@ -550,7 +583,7 @@ __global__ void __launch_bounds__(MAXT) __attribute__((amdgpu_waves_per_eu(K == 
         for (int k = 0; k < K; ++k) ay[k] = top[k];                                                                   \
       }                                                                                                               \
       if (x >= 0) {                                                                                                   \
-        const int mx = st[ST_MX];                                                                                     \
+        const int mx = st.mx;                                                                                     \
       _Pragma("unroll")                                                                                               \
         for (int k = 0; k < K; ++k) ax[k] = look(mx, tipb(x, k));                                                     \
       } else if (y >= 0) {                                                                                            \
@@ -558,7 +591,7 @@ __global__ void __launch_bounds__(MAXT) __attribute__((amdgpu_waves_per_eu(K == 
         for (int k = 0; k < K; ++k) ax[k] = top[k];                                                                   \
       } else {                                                                                                        \
         {                                                                                                             \
-          const int xd = st[ST_XDPOS];                                                                                \
+          const int xd = st.xd;                                                                                \
           if (DL || xd < ndl) {                                                                                       \
       _Pragma("unroll")                                                                                               \
             for (int k = 0; k < K; ++k) ax[k] = dget(xd, k);                                                          \
@@ -573,7 +606,7 @@ __global__ void __launch_bounds__(MAXT) __attribute__((amdgpu_waves_per_eu(K == 
       if (vs >= 0) {                                                                                                  \
         V4 av[K];                                                                                                     \
         if (fl & F_MV) {                                                                                              \
-          pvec_k<K>(mrec(st[ST_MV]), pv, av);                                                                         \
+          pvec_k<K>(mrec(st.mv), pv, av);                                                                         \
         } else { /* merged root branch of an unrooted tree: identity */                                                \
       _Pragma("unroll")                                                                                               \
           for (int k = 0; k < K; ++k) av[k] = pv[k];                                                                  \
@@ -581,7 +614,7 @@ __global__ void __launch_bounds__(MAXT) __attribute__((amdgpu_waves_per_eu(K == 
       _Pragma("unroll")                                                                                               \
         for (int k = 0; k < K; ++k) if (!(PHY_ABLATE & 8)) st_v4(srd_scr, soff(vs, k), half_bytes, av[k]);                                    \
         if (fl & F_VDEEP) {                                                                                           \
-          const int dp = st[ST_VDPOS];                                                                                \
+          const int dp = st.vd;                                                                                \
           if (DL || dp < ndl)  /* a global entry is x's scratch slot itself */                                        \
           for (int k = 0; k < K; ++k) dput(dp, k, av[k]);                                                             \
         }                                                                                                             \
@@ -596,10 +629,11 @@ __global__ void __launch_bounds__(MAXT) __attribute__((amdgpu_waves_per_eu(K == 
       V4 dA[K], dB[K];
 #pragma unroll
       for (int k = 0; k < K; ++k) dA[k] = {0.0, 0.0, 0.0, 0.0};  // step 0 has no internal child
+      Step sA = ld_step(prog, 0), sB;
       for (int s = 0;;) {
-        FSTEP(s, dA, dB);
+        FSTEP(s, dA, dB, sA, sB);
         if (++s >= nsteps) break;
-        FSTEP(s, dB, dA);
+        FSTEP(s, dB, dA, sB, sA);
         if (++s >= nsteps) break;
       }
     }
@@ -650,14 +684,15 @@ __global__ void __launch_bounds__(MAXT) __attribute__((amdgpu_waves_per_eu(K == 
     // one step ahead (zeros for tips: out-of-range offset).
     struct CSet {
       V4 lx[K], ly[K], lr[K];
+      Step st;  // the step's record, loaded with its operands
     };
     #define LOAD_SET(s, r) do {                                                  \
       const bool ok = s >= 0;                                                    \
-      const int* sp = prog + (ok ? s : 0) * STEP_INTS;                           \
-      const int x = sp[ST_X], y = sp[ST_Y], fl = sp[ST_FLAGS];                   \
-      const bool lx = ok && x < 0, ly = ok && y < 0;                             \
-      const bool lr = ok && (fl & F_VDEEP) && sp[ST_VDPOS] >= ndl;               \
-      const int xs = sp[ST_XSLOT], ys = sp[ST_YSLOT], vd = sp[ST_VDPOS];         \
+      r.st = ld_step(prog, ok ? s : 0);                                   \
+      const int x = r.st.x, y = r.st.y, fl = r.st.fl;                     \
+      const bool lx = ok && x < 0, ly = ok && y < 0;                      \
+      const bool lr = ok && (fl & F_VDEEP) && r.st.vd >= ndl;             \
+      const int xs = r.st.xs, ys = r.st.ys, vd = r.st.vd;                 \
       _Pragma("unroll")                                                          \
       for (int k = 0; k < K; ++k) {                                              \
         r.lx[k] = ld_v4(srd_scr, lx ? soff(xs, k) : scr_bytes, half_bytes);      \
@@ -667,13 +702,13 @@ __global__ void __launch_bounds__(MAXT) __attribute__((amdgpu_waves_per_eu(K == 
       }                                                                          \
     } while (0)
     #define RSTEP(s, cs) do {                                                       \
-      const int* st = prog + s * STEP_INTS;                                         \
+      const Step& st = cs.st;                                                       \
       ensure_chunk(st);                                                             \
-      const int x = st[ST_X], y = st[ST_Y], fl = st[ST_FLAGS];                      \
+      const int x = st.x, y = st.y, fl = st.fl;                      \
       V4 rv[K], ax[K], ay[K], q[K], rx[K], ry[K];                                   \
       unsigned bx[K], by[K];                                                        \
       if (fl & F_VDEEP) {                                                           \
-        const int vd = st[ST_VDPOS];                                                \
+        const int vd = st.vd;                                                \
         if (DL || vd < ndl) {                                                       \
       _Pragma("unroll")                                                             \
           for (int k = 0; k < K; ++k) rv[k] = dget(vd, k);                          \
@@ -686,7 +721,7 @@ __global__ void __launch_bounds__(MAXT) __attribute__((amdgpu_waves_per_eu(K == 
         for (int k = 0; k < K; ++k) rv[k] = topr[k];                                \
       }                                                                             \
       if (x >= 0) {                                                                 \
-        const int mx = st[ST_MX];                                                   \
+        const int mx = st.mx;                                                   \
       _Pragma("unroll")                                                             \
         for (int k = 0; k < K; ++k) {                                               \
           bx[k] = tipb(x, k);                                                       \
@@ -697,7 +732,7 @@ __global__ void __launch_bounds__(MAXT) __attribute__((amdgpu_waves_per_eu(K == 
         for (int k = 0; k < K; ++k) ax[k] = cs.lx[k];                               \
       }                                                                             \
       if (y >= 0) {                                                                 \
-        const int my = st[ST_MY];                                                   \
+        const int my = st.my;                                                   \
       _Pragma("unroll")                                                             \
         for (int k = 0; k < K; ++k) {                                               \
           by[k] = tipb(y, k);                                                       \
@@ -708,7 +743,7 @@ __global__ void __launch_bounds__(MAXT) __attribute__((amdgpu_waves_per_eu(K == 
         for (int k = 0; k < K; ++k) ay[k] = cs.ly[k];                               \
       }                                                                             \
       if (fl & F_MV) {                                                              \
-        const int mv = st[ST_MV];                                                   \
+        const int mv = st.mv;                                                   \
         V4 pv[K];                                                                   \
       _Pragma("unroll")                                                             \
         for (int k = 0; k < K; ++k) pv[k] = vmul(ax[k], ay[k]);                     \
@@ -727,16 +762,16 @@ __global__ void __launch_bounds__(MAXT) __attribute__((amdgpu_waves_per_eu(K == 
         V4 tv[K];                                                                   \
       _Pragma("unroll")                                                             \
         for (int k = 0; k < K; ++k) tv[k] = tipvec_b(bx[k], a.extra);                        \
-        gacc(st[ST_MX], rx, tv);                                                    \
+        gacc(st.mx, rx, tv);                                                    \
       }                                                                             \
       if (y >= 0) {                                                                 \
         V4 tv[K];                                                                   \
       _Pragma("unroll")                                                             \
         for (int k = 0; k < K; ++k) tv[k] = tipvec_b(by[k], a.extra);                        \
-        gacc(st[ST_MY], ry, tv);                                                    \
+        gacc(st.my, ry, tv);                                                    \
       }                                                                             \
       if (x < 0 && y < 0) { /* r_x waits on the deep stack while y's subtree runs */ \
-        const int dp = st[ST_XDPOS];                                                \
+        const int dp = st.xd;                                                \
       _Pragma("unroll")                                                             \
         for (int k = 0; k < K; ++k) {                                               \
           if (DL || dp < ndl) dput(dp, k, rx[k]); else put(dsk, dp, k, rx[k]);  \
@@ -1218,6 +1253,26 @@ void free_ctx(phy_ctx* c) {
 // only the first child x of a node whose children are both internal waits
 // while y's subtree runs.  Those waits nest, so they live on a stack whose
 // entry per wait is fixed here (ST_XDPOS / ST_VDPOS), used by both passes.
+// Device layout of the program (see Step / ld_step): 8 packed ints per step.
+std::vector<int> pack_program(const std::vector<int>& prog) {
+  const size_t n = prog.size() / STEP_INTS;
+  std::vector<int> out(n * PSTEP, 0);
+  auto h = [](int lo, int hi) { return (int)(((unsigned)(lo & 0xFFFF)) | ((unsigned)hi << 16)); };
+  for (size_t s = 0; s < n; ++s) {
+    const int* p = &prog[s * STEP_INTS];
+    int* q = &out[s * PSTEP];
+    q[0] = h(p[ST_X], p[ST_Y]);
+    q[1] = h(p[ST_MX], p[ST_MY]);
+    q[2] = h(p[ST_MV], p[ST_VSLOT]);
+    q[3] = h(p[ST_XSLOT], p[ST_YSLOT]);
+    q[4] = (int)((unsigned)(p[ST_FLAGS] & 0xFF) | ((unsigned)(p[ST_XDPOS] & 0xFF) << 8) |
+                 ((unsigned)(p[ST_VDPOS] & 0xFF) << 16));
+    q[5] = h(p[ST_CHUNK], p[ST_M0]);
+    q[6] = h(p[ST_MN], p[ST_NODE]);
+  }
+  return out;
+}
+
 int build_program(int S, const int32_t* peel, int rooted, std::vector<int>& prog,
                   std::vector<int>& mat_branch, int& nslots, int& ndeep) {
   const int N = 2 * S - 1;
@@ -1455,7 +1510,10 @@ int plan_chunks(phy_ctx* c) {
     const int m1 = (k < ch) ? c->prog[(size_t)first_step[k + 1] * STEP_INTS + ST_M0] : c->nmat;
     for (int s = first_step[k]; s < first_step[k + 1]; ++s) c->prog[(size_t)s * STEP_INTS + ST_MN] = m1 - m0;
   }
-  HIP_TRY(hipMemcpy(c->d_prog, c->prog.data(), c->prog.size() * sizeof(int), hipMemcpyHostToDevice));
+  {
+    const std::vector<int> packed = pack_program(c->prog);
+    HIP_TRY(hipMemcpy(c->d_prog, packed.data(), packed.size() * sizeof(int), hipMemcpyHostToDevice));
+  }
   c->cap_m = cap;
   c->nchunks = ch + 1;
   c->deep_lds = ndl > 0 && ndl == c->ndeep;
@@ -1571,6 +1629,10 @@ int phy_create(int S, int P, int C, int rooted, int model, const uint8_t* tipcod
   }
   c->nsteps = S - 1;
   c->nmat = (int)mat_branch.size();
+  if (S > 16000 || c->ndeep > 127) {  // the packed device program's field widths
+    delete c;
+    return fail(PHY_EINVAL, "tree too large for the packed program (S <= 16000, deep stack <= 127)");
+  }
   // matrix records: 4 columns + P t for every non-one-hot mask t in the data
   // (15 always: the padding patterns' mask)
   std::vector<int> vec_of(16, -1);
@@ -1686,7 +1748,10 @@ int phy_create(int S, int P, int C, int rooted, int model, const uint8_t* tipcod
       }
     HIP_C(hipMemcpy(c->d_tips, tips.data(), tips.size(), hipMemcpyHostToDevice));
     HIP_C(hipMemcpy(c->d_w, w.data(), w.size() * sizeof(double), hipMemcpyHostToDevice));
-    HIP_C(hipMemcpy(c->d_prog, c->prog.data(), c->prog.size() * sizeof(int), hipMemcpyHostToDevice));
+    {
+      const std::vector<int> packed = pack_program(c->prog);
+      HIP_C(hipMemcpy(c->d_prog, packed.data(), packed.size() * sizeof(int), hipMemcpyHostToDevice));
+    }
     HIP_C(hipMemcpy(c->d_mat_branch, mat_branch.data(), mat_branch.size() * sizeof(int), hipMemcpyHostToDevice));
     HIP_C(hipMemcpy(c->d_gpos, gpos.data(), gpos.size() * sizeof(int), hipMemcpyHostToDevice));
   }
