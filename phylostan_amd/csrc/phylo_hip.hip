@@ -288,10 +288,14 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* base, ui
   void* p = reinterpret_cast<void*>(((uint64_t)hi << 32) | lo);
   return __builtin_amdgcn_make_buffer_rsrc(p, (short)0, (int)n, 0x00020000);
 }
-// One stored 4-vector: two 16-B halves `half` bytes apart.
+// One stored 4-vector: two 16-B halves `half` bytes apart.  Every stored
+// partial is read exactly once, so the loads are non-temporal (aux 2 = nt):
+// measured +13% (fluA) / +3% (synthetic) over the default policy, with the
+// stores left at the default (nt or sc1 stores measured no better).
+constexpr int LOAD_NT = 2;
 __device__ __forceinline__ V4 ld_v4(__amdgpu_buffer_rsrc_t srd, uint32_t off, uint32_t half) {
-  const auto lo = __builtin_amdgcn_raw_buffer_load_b128(srd, off, 0, 0);
-  const auto hi = __builtin_amdgcn_raw_buffer_load_b128(srd, off + half, 0, 0);
+  const auto lo = __builtin_amdgcn_raw_buffer_load_b128(srd, off, 0, LOAD_NT);
+  const auto hi = __builtin_amdgcn_raw_buffer_load_b128(srd, off + half, 0, LOAD_NT);
   V4 r;
   r.x = __hiloint2double((int)lo[1], (int)lo[0]);
   r.y = __hiloint2double((int)lo[3], (int)lo[2]);
