@@ -705,89 +705,99 @@ __global__ void __launch_bounds__(MAXT) __attribute__((amdgpu_waves_per_eu(K == 
           r.lr[k] = ld_v4(srd_dsk, lr ? eoff(vd, k) : dsk_bytes, half_bytes);    \
       }                                                                          \
     } while (0)
-    #define RSTEP(s, cs) do {                                                       \
-      const Step& st = cs.st;                                                       \
-      ensure_chunk(st);                                                             \
-      const int x = st.x, y = st.y, fl = st.fl;                      \
-      V4 rv[K], ax[K], ay[K], q[K], rx[K], ry[K];                                   \
-      unsigned bx[K], by[K];                                                        \
-      if (fl & F_VDEEP) {                                                           \
-        const int vd = st.vd;                                                \
-        if (DL || vd < ndl) {                                                       \
-      _Pragma("unroll")                                                             \
-          for (int k = 0; k < K; ++k) rv[k] = dget(vd, k);                          \
-        } else {                                                                    \
-      _Pragma("unroll")                                                             \
-          for (int k = 0; k < K; ++k) rv[k] = cs.lr[k];                             \
-        }                                                                           \
-      } else {                                                                      \
-      _Pragma("unroll")                                                             \
-        for (int k = 0; k < K; ++k) rv[k] = topr[k];                                \
-      }                                                                             \
-      if (x >= 0) {                                                                 \
-        const int mx = st.mx;                                                   \
-      _Pragma("unroll")                                                             \
-        for (int k = 0; k < K; ++k) {                                               \
-          bx[k] = tipb(x, k);                                                       \
-          ax[k] = look(mx, bx[k]);                                                  \
-        }                                                                           \
-      } else {                                                                      \
-      _Pragma("unroll")                                                             \
-        for (int k = 0; k < K; ++k) ax[k] = cs.lx[k];                               \
-      }                                                                             \
-      if (y >= 0) {                                                                 \
-        const int my = st.my;                                                   \
-      _Pragma("unroll")                                                             \
-        for (int k = 0; k < K; ++k) {                                               \
-          by[k] = tipb(y, k);                                                       \
-          ay[k] = look(my, by[k]);                                                  \
-        }                                                                           \
-      } else {                                                                      \
-      _Pragma("unroll")                                                             \
-        for (int k = 0; k < K; ++k) ay[k] = cs.ly[k];                               \
-      }                                                                             \
-      if (fl & F_MV) {                                                              \
-        const int mv = st.mv;                                                   \
-        V4 pv[K];                                                                   \
-      _Pragma("unroll")                                                             \
-        for (int k = 0; k < K; ++k) pv[k] = vmul(ax[k], ay[k]);                     \
-        ptvec_k<K>(mrec(mv), rv, q);                                                \
-        gacc(mv, rv, pv); /* dL/dP_v += r_v (x) p_v */                               \
-      } else { /* root, or the merged root branch: identity */                       \
-      _Pragma("unroll")                                                             \
-        for (int k = 0; k < K; ++k) q[k] = rv[k];                                   \
-      }                                                                             \
-      _Pragma("unroll")                                                             \
-      for (int k = 0; k < K; ++k) {                                                 \
-        rx[k] = vmul(q[k], ay[k]);                                                  \
-        ry[k] = vmul(q[k], ax[k]);                                                  \
-      }                                                                             \
-      if (x >= 0) {                                                                 \
-        V4 tv[K];                                                                   \
-      _Pragma("unroll")                                                             \
-        for (int k = 0; k < K; ++k) tv[k] = tipvec_b(bx[k], a.extra);                        \
-        gacc(st.mx, rx, tv);                                                    \
-      }                                                                             \
-      if (y >= 0) {                                                                 \
-        V4 tv[K];                                                                   \
-      _Pragma("unroll")                                                             \
-        for (int k = 0; k < K; ++k) tv[k] = tipvec_b(by[k], a.extra);                        \
-        gacc(st.my, ry, tv);                                                    \
-      }                                                                             \
-      if (x < 0 && y < 0) { /* r_x waits on the deep stack while y's subtree runs */ \
-        const int dp = st.xd;                                                \
-      _Pragma("unroll")                                                             \
-        for (int k = 0; k < K; ++k) {                                               \
-          if (DL || dp < ndl) dput(dp, k, rx[k]); else put(dsk, dp, k, rx[k]);  \
-          topr[k] = ry[k];                                                          \
-        }                                                                           \
-      } else if (y < 0) {                                                           \
-      _Pragma("unroll")                                                             \
-        for (int k = 0; k < K; ++k) topr[k] = ry[k];                                \
-      } else if (x < 0) {                                                           \
-      _Pragma("unroll")                                                             \
-        for (int k = 0; k < K; ++k) topr[k] = rx[k];                                \
-      }                                                                             \
+    #define RSTEP_V(s, cs, XT, YT) do {                                           \
+      const Step& st = cs.st;                                                     \
+      ensure_chunk(st);                                                           \
+      const int fl = st.fl;                                                       \
+      V4 rv[K], ax[K], ay[K], q[K], rx[K], ry[K];                                 \
+      unsigned bx[K], by[K];                                                      \
+      if (fl & F_VDEEP) {                                                         \
+        const int vd = st.vd;                                                     \
+        if (DL || vd < ndl) {                                                     \
+      _Pragma("unroll")                                                           \
+          for (int k = 0; k < K; ++k) rv[k] = dget(vd, k);                        \
+        } else {                                                                  \
+      _Pragma("unroll")                                                           \
+          for (int k = 0; k < K; ++k) rv[k] = cs.lr[k];                           \
+        }                                                                         \
+      } else {                                                                    \
+      _Pragma("unroll")                                                           \
+        for (int k = 0; k < K; ++k) rv[k] = topr[k];                              \
+      }                                                                           \
+      if (XT) {                                                                   \
+        const int mx = st.mx, x = st.x;                                           \
+      _Pragma("unroll")                                                           \
+        for (int k = 0; k < K; ++k) {                                             \
+          bx[k] = tipb(x, k);                                                     \
+          ax[k] = look(mx, bx[k]);                                                \
+        }                                                                         \
+      } else {                                                                    \
+      _Pragma("unroll")                                                           \
+        for (int k = 0; k < K; ++k) ax[k] = cs.lx[k];                             \
+      }                                                                           \
+      if (YT) {                                                                   \
+        const int my = st.my, y = st.y;                                           \
+      _Pragma("unroll")                                                           \
+        for (int k = 0; k < K; ++k) {                                             \
+          by[k] = tipb(y, k);                                                     \
+          ay[k] = look(my, by[k]);                                                \
+        }                                                                         \
+      } else {                                                                    \
+      _Pragma("unroll")                                                           \
+        for (int k = 0; k < K; ++k) ay[k] = cs.ly[k];                             \
+      }                                                                           \
+      if (fl & F_MV) {                                                            \
+        const int mv = st.mv;                                                     \
+        V4 pv[K];                                                                 \
+      _Pragma("unroll")                                                           \
+        for (int k = 0; k < K; ++k) pv[k] = vmul(ax[k], ay[k]);                   \
+        ptvec_k<K>(mrec(mv), rv, q);                                              \
+        gacc(mv, rv, pv); /* dL/dP_v += r_v (x) p_v */                            \
+      } else { /* root, or the merged root branch: identity */                    \
+      _Pragma("unroll")                                                           \
+        for (int k = 0; k < K; ++k) q[k] = rv[k];                                 \
+      }                                                                           \
+      _Pragma("unroll")                                                           \
+      for (int k = 0; k < K; ++k) {                                               \
+        rx[k] = vmul(q[k], ay[k]);                                                \
+        ry[k] = vmul(q[k], ax[k]);                                                \
+      }                                                                           \
+      if (XT) {                                                                   \
+        V4 tv[K];                                                                 \
+      _Pragma("unroll")                                                           \
+        for (int k = 0; k < K; ++k) tv[k] = tipvec_b(bx[k], a.extra);             \
+        gacc(st.mx, rx, tv);                                                      \
+      }                                                                           \
+      if (YT) {                                                                   \
+        V4 tv[K];                                                                 \
+      _Pragma("unroll")                                                           \
+        for (int k = 0; k < K; ++k) tv[k] = tipvec_b(by[k], a.extra);             \
+        gacc(st.my, ry, tv);                                                      \
+      }                                                                           \
+      if (!XT && !YT) { /* r_x waits on the deep stack while y's subtree runs */  \
+        const int dp = st.xd;                                                     \
+      _Pragma("unroll")                                                           \
+        for (int k = 0; k < K; ++k) {                                             \
+          if (DL || dp < ndl) dput(dp, k, rx[k]); else put(dsk, dp, k, rx[k]);    \
+          topr[k] = ry[k];                                                        \
+        }                                                                         \
+      } else if (!YT) {                                                           \
+      _Pragma("unroll")                                                           \
+        for (int k = 0; k < K; ++k) topr[k] = ry[k];                              \
+      } else if (!XT) {                                                           \
+      _Pragma("unroll")                                                           \
+        for (int k = 0; k < K; ++k) topr[k] = rx[k];                              \
+      }                                                                           \
+    } while (0)
+    /* one straight-line body per child kind (tip / internal), so the
+       independent LDS reads and dL/dP reductions of a step share a basic
+       block and the scheduler can interleave them */
+    #define RSTEP(s, cs) do {                                                 \
+      const int xt_ = cs.st.x >= 0, yt_ = cs.st.y >= 0;                       \
+      if (xt_ && yt_) RSTEP_V(s, cs, true, true);                             \
+      else if (xt_) RSTEP_V(s, cs, true, false);                              \
+      else if (yt_) RSTEP_V(s, cs, false, true);                              \
+      else RSTEP_V(s, cs, false, false);                                      \
     } while (0)
     if (!(PHY_ABLATE & 2)) {
       int s = nsteps - 1;
