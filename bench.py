@@ -91,10 +91,11 @@ def synthetic_problem(sites):
 
 
 def algorithmic_bytes(S, P, C, nslots, B, draws):
-    """HBM bytes one sweep launch must move (DESIGN.md "Roofline"):
-    every non-root internal partial written once + read once (2 x 32 B per
-    slot per column), tip codes (S/2 B/pattern: 4-bit record indices),
-    weights (8 B/pattern), P-matrices in + dL/dP out (2 x 128 B per
+    """HBM bytes one sweep launch must move (DESIGN.md "Roofline"): every
+    stored moved partial written once + read once (2 x 32 B per stored slot
+    per column; ``nslots`` = the slots the plan stores, i.e. non-root internal
+    nodes minus recomputed cherries), tip codes (S/2 B/pattern: 4-bit record
+    indices), weights (8 B/pattern), P-matrices in + dL/dP out (2 x 128 B per
     branch-category)."""
     per_draw = 64 * nslots * C * P + S * P // 2 + 8 * P + 256 * B * C
     return per_draw * draws
@@ -238,7 +239,7 @@ def main():
         tb = time.perf_counter()
         single = dict(evals_per_s=n1 / (tb - ta), us_per_eval=1e6 * (tb - ta) / n1)
 
-    alg = algorithmic_bytes(S, P_local, C, info["nslots"], B, draws)
+    alg = algorithmic_bytes(S, P_local, C, info["nslots"] - info.get("recomputed", 0), B, draws)
     achieved = alg / (kern_avg_ms * 1e-3) / 1e9
     traffic = None
     pmc = os.path.join(ROOT, "profiles", "pmc_traffic.json")

@@ -154,6 +154,16 @@ int phy_columns_per_lane(const phy_ctx* ctx);
 int phy_set_deep_stack(phy_ctx* ctx, int mode);
 int phy_deep_stack_in_lds(const phy_ctx* ctx);
 
+/* Recomputed cherries (default on; PHY_RECOMPUTE=0 at phy_create turns it
+ * off): a node whose two children are tips, computed by the step just before
+ * its parent's and in the same LDS chunk, is not written to scratch in the
+ * forward half; the parent's reverse step rebuilds it from LDS.  Results are
+ * identical either way (same operations in the same order).
+ * phy_recomputed_partials: moved partials per column the current plan does
+ * not store. */
+int phy_set_recompute(phy_ctx* ctx, int on);
+int phy_recomputed_partials(const phy_ctx* ctx);
+
 #ifdef __cplusplus
 }
 #endif

@@ -43,6 +43,8 @@ SIGNATURES = {
     "phy_columns_per_lane": (ctypes.c_int, [ctypes.c_void_p]),
     "phy_set_deep_stack": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
     "phy_deep_stack_in_lds": (ctypes.c_int, [ctypes.c_void_p]),
+    "phy_set_recompute": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
+    "phy_recomputed_partials": (ctypes.c_int, [ctypes.c_void_p]),
 }
 
 

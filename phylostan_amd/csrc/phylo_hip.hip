@@ -80,6 +80,13 @@ enum {
 constexpr int F_MV = 1;     // the step's branch has a matrix (else identity)
 constexpr int F_XDEEP = 2;  // both children internal: x's operand is on the deep stack
 constexpr int F_VDEEP = 4;  // v is the x child of a both-internal parent
+// Recomputed cherries (set per LDS plan, plan_chunks): a node whose children
+// are both tips is not stored when it is the previous step of its parent and
+// shares the parent's LDS chunk -- the parent's reverse step rebuilds it from
+// the tips and matrices already in LDS (its step record is the one the
+// reverse loaded a step ahead).
+constexpr int F_NOSTORE = 8;   // this step's a_v is not written to scratch
+constexpr int F_PREVREC = 16;  // the child computed at the previous step is rebuilt, not loaded
 
 // The device copy of the program packs a step into 8 ints (pack_program):
 //   w0 x | y<<16   w1 mx | my<<16   w2 mv | vslot<<16   w3 xslot | yslot<<16
@@ -616,7 +623,7 @@ __global__ void __launch_bounds__(MAXT) __attribute__((amdgpu_waves_per_eu(K == 
           for (int k = 0; k < K; ++k) av[k] = pv[k];                                                                  \
         }                                                                                                             \
       _Pragma("unroll")                                                                                               \
-        for (int k = 0; k < K; ++k) if (!(PHY_ABLATE & 8)) st_v4(srd_scr, soff(vs, k), half_bytes, av[k]);                                    \
+        for (int k = 0; k < K; ++k) if (!(PHY_ABLATE & 8) && !(fl & F_NOSTORE)) st_v4(srd_scr, soff(vs, k), half_bytes, av[k]);                                    \
         if (fl & F_VDEEP) {                                                                                           \
           const int dp = st.vd;                                                                                \
           if (DL || dp < ndl)  /* a global entry is x's scratch slot itself */                                        \
@@ -694,7 +701,10 @@ __global__ void __launch_bounds__(MAXT) __attribute__((amdgpu_waves_per_eu(K == 
       const bool ok = s >= 0;                                                    \
       r.st = ld_step(prog, ok ? s : 0);                                   \
       const int x = r.st.x, y = r.st.y, fl = r.st.fl;                     \
-      const bool lx = ok && x < 0, ly = ok && y < 0;                      \
+      /* a rebuilt cherry (F_PREVREC) is the previous-step child: y when y is       \
+         internal, else x -- its operand is not loaded */                           \
+      const bool rec_ = fl & F_PREVREC;                                             \
+      const bool lx = ok && x < 0 && !(rec_ && y >= 0), ly = ok && y < 0 && !rec_;  \
       const bool lr = ok && (fl & F_VDEEP) && r.st.vd >= ndl;             \
       const int xs = r.st.xs, ys = r.st.ys, vd = r.st.vd;                 \
       _Pragma("unroll")                                                          \
@@ -705,7 +715,14 @@ __global__ void __launch_bounds__(MAXT) __attribute__((amdgpu_waves_per_eu(K == 
           r.lr[k] = ld_v4(srd_dsk, lr ? eoff(vd, k) : dsk_bytes, half_bytes);    \
       }                                                                          \
     } while (0)
-    #define RSTEP_V(s, cs, XT, YT) do {                                           \
+    #define REBUILD(cst, out) do { /* a_c of a cherry c from LDS, as its forward step formed it */  \
+      V4 p_[K];                                                                                     \
+      _Pragma("unroll")                                                                             \
+      for (int k = 0; k < K; ++k)                                                                   \
+        p_[k] = vmul(look(cst.mx, tipb(cst.x, k)), look(cst.my, tipb(cst.y, k)));                   \
+      pvec_k<K>(mrec(cst.mv), p_, out);                                                             \
+    } while (0)
+    #define RSTEP_V(s, cs, cn, XT, YT) do {                                                         \
       const Step& st = cs.st;                                                     \
       ensure_chunk(st);                                                           \
       const int fl = st.fl;                                                       \
@@ -731,9 +748,11 @@ __global__ void __launch_bounds__(MAXT) __attribute__((amdgpu_waves_per_eu(K == 
           bx[k] = tipb(x, k);                                                     \
           ax[k] = look(mx, bx[k]);                                                \
         }                                                                         \
-      } else {                                                                    \
-      _Pragma("unroll")                                                           \
-        for (int k = 0; k < K; ++k) ax[k] = cs.lx[k];                             \
+      } else if (YT && (fl & F_PREVREC)) { /* x is the rebuilt previous-step child */  \
+        REBUILD(cn.st, ax);                                                            \
+      } else {                                                                         \
+      _Pragma("unroll")                                                                \
+        for (int k = 0; k < K; ++k) ax[k] = cs.lx[k];                                  \
       }                                                                           \
       if (YT) {                                                                   \
         const int my = st.my, y = st.y;                                           \
@@ -742,9 +761,11 @@ __global__ void __launch_bounds__(MAXT) __attribute__((amdgpu_waves_per_eu(K == 
           by[k] = tipb(y, k);                                                     \
           ay[k] = look(my, by[k]);                                                \
         }                                                                         \
-      } else {                                                                    \
-      _Pragma("unroll")                                                           \
-        for (int k = 0; k < K; ++k) ay[k] = cs.ly[k];                             \
+      } else if (fl & F_PREVREC) { /* y is the rebuilt previous-step child */  \
+        REBUILD(cn.st, ay);                                                    \
+      } else {                                                                 \
+      _Pragma("unroll")                                                        \
+        for (int k = 0; k < K; ++k) ay[k] = cs.ly[k];                          \
       }                                                                           \
       if (fl & F_MV) {                                                            \
         const int mv = st.mv;                                                     \
@@ -792,12 +813,12 @@ __global__ void __launch_bounds__(MAXT) __attribute__((amdgpu_waves_per_eu(K == 
     /* one straight-line body per child kind (tip / internal), so the
        independent LDS reads and dL/dP reductions of a step share a basic
        block and the scheduler can interleave them */
-    #define RSTEP(s, cs) do {                                                 \
-      const int xt_ = cs.st.x >= 0, yt_ = cs.st.y >= 0;                       \
-      if (xt_ && yt_) RSTEP_V(s, cs, true, true);                             \
-      else if (xt_) RSTEP_V(s, cs, true, false);                              \
-      else if (yt_) RSTEP_V(s, cs, false, true);                              \
-      else RSTEP_V(s, cs, false, false);                                      \
+    #define RSTEP(s, cs, cn) do {                        \
+      const int xt_ = cs.st.x >= 0, yt_ = cs.st.y >= 0;  \
+      if (xt_ && yt_) RSTEP_V(s, cs, cn, true, true);    \
+      else if (xt_) RSTEP_V(s, cs, cn, true, false);     \
+      else if (yt_) RSTEP_V(s, cs, cn, false, true);     \
+      else RSTEP_V(s, cs, cn, false, false);             \
     } while (0)
     if (!(PHY_ABLATE & 2)) {
       int s = nsteps - 1;
@@ -805,10 +826,10 @@ __global__ void __launch_bounds__(MAXT) __attribute__((amdgpu_waves_per_eu(K == 
       LOAD_SET(s, A);
       for (;;) {
         LOAD_SET(s - 1, Bs);
-        RSTEP(s, A);
+        RSTEP(s, A, Bs);
         if (--s < 0) break;
         LOAD_SET(s - 1, A);
-        RSTEP(s, Bs);
+        RSTEP(s, Bs, A);
         if (--s < 0) break;
       }
     }
@@ -1213,6 +1234,8 @@ struct phy_ctx {
   int deep_pref = 0;           // deep stack: 0 automatic, 1 LDS, 2 global
   bool deep_lds = false;       // current plan keeps the whole deep stack in LDS
   int ndl = 0;                 // deep entries in LDS (== ndeep when deep_lds)
+  bool recompute = true;       // rebuild cherries in the reverse instead of storing them
+  int nrec = 0;                // cherries recomputed under the current plan
   hipStream_t stream;
   std::vector<int> prog;  // host copy of the program (chunk fields per plan)
   uint8_t* d_tips = nullptr;
@@ -1524,6 +1547,23 @@ int plan_chunks(phy_ctx* c) {
     const int m1 = (k < ch) ? c->prog[(size_t)first_step[k + 1] * STEP_INTS + ST_M0] : c->nmat;
     for (int s = first_step[k]; s < first_step[k + 1]; ++s) c->prog[(size_t)s * STEP_INTS + ST_MN] = m1 - m0;
   }
+  // recomputed cherries (F_NOSTORE / F_PREVREC), valid for this chunk plan
+  c->nrec = 0;
+  for (int s = 0; s < c->nsteps; ++s) c->prog[(size_t)s * STEP_INTS + ST_FLAGS] &= ~(F_NOSTORE | F_PREVREC);
+  if (c->recompute) {
+    for (int s = 1; s < c->nsteps; ++s) {
+      int* p = &c->prog[(size_t)s * STEP_INTS];
+      int* q = &c->prog[(size_t)(s - 1) * STEP_INTS];
+      const bool has_internal = p[ST_X] < 0 || p[ST_Y] < 0;  // then step s-1 is its top child
+      const bool cherry = q[ST_X] >= 0 && q[ST_Y] >= 0 && (q[ST_FLAGS] & F_MV) && q[ST_VSLOT] >= 0 &&
+                          !(q[ST_FLAGS] & F_VDEEP);
+      if (has_internal && cherry && p[ST_CHUNK] == q[ST_CHUNK]) {
+        q[ST_FLAGS] |= F_NOSTORE;
+        p[ST_FLAGS] |= F_PREVREC;
+        ++c->nrec;
+      }
+    }
+  }
   {
     const std::vector<int> packed = pack_program(c->prog);
     HIP_TRY(hipMemcpy(c->d_prog, packed.data(), packed.size() * sizeof(int), hipMemcpyHostToDevice));
@@ -1673,6 +1713,8 @@ int phy_create(int S, int P, int C, int rooted, int model, const uint8_t* tipcod
     c->cols_pref = ck ? std::max(0, std::min(2, atoi(ck))) : 0;
     const char* dk = getenv("PHY_DEEP");
     c->deep_pref = dk ? std::max(0, std::min(2, atoi(dk))) : 0;
+    const char* rk = getenv("PHY_RECOMPUTE");
+    c->recompute = rk ? atoi(rk) != 0 : true;
   }
   hipError_t he = hipSetDevice(device);
   if (he != hipSuccess) {
@@ -1898,6 +1940,14 @@ int phy_set_deep_stack(phy_ctx* ctx, int mode) {
   return plan_chunks(ctx);
 }
 int phy_deep_stack_in_lds(const phy_ctx* ctx) { return ctx ? ctx->ndl : -1; }
+
+int phy_set_recompute(phy_ctx* ctx, int on) {
+  if (!ctx) return fail(PHY_EINVAL, "NULL ctx");
+  ctx->recompute = on != 0;
+  HIP_TRY(hipSetDevice(ctx->device));
+  return plan_chunks(ctx);
+}
+int phy_recomputed_partials(const phy_ctx* ctx) { return ctx ? ctx->nrec : -1; }
 
 int phy_lds_plan(const phy_ctx* ctx, int* n_chunks, int* matrices_per_chunk, int* lds_bytes_out) {
   if (!ctx) return fail(PHY_EINVAL, "NULL ctx");

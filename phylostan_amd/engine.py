@@ -165,12 +165,17 @@ class TreeLikelihood:
         """Deep-stack placement: 0 automatic, 1 LDS, 2 global (replans)."""
         _lib.check(self.lib.phy_set_deep_stack(self.ctx, int(mode)), "phy_set_deep_stack")
 
+    def set_recompute(self, on=True):
+        """Rebuild cherries in the reverse half instead of storing them (replans)."""
+        _lib.check(self.lib.phy_set_recompute(self.ctx, int(bool(on))), "phy_set_recompute")
+
     def lds_plan(self):
         vals = [ctypes.c_int() for _ in range(3)]
         _lib.check(self.lib.phy_lds_plan(self.ctx, *[ctypes.byref(v) for v in vals]), "phy_lds_plan")
         out = dict(zip(("n_chunks", "matrices_per_chunk", "lds_bytes"), [v.value for v in vals]))
         out["cols"] = self.lib.phy_columns_per_lane(self.ctx)
         out["deep_lds_entries"] = self.lib.phy_deep_stack_in_lds(self.ctx)
+        out["recomputed"] = self.lib.phy_recomputed_partials(self.ctx)
         return out
 
     def timing_start(self):
