@@ -87,6 +87,8 @@ constexpr int F_VDEEP = 4;  // v is the x child of a both-internal parent
 // reverse loaded a step ahead).
 constexpr int F_NOSTORE = 8;   // this step's a_v is not written to scratch
 constexpr int F_PREVREC = 16;  // the child computed at the previous step is rebuilt, not loaded
+constexpr int F_PREVREC2 = 32; // ... and that child (one tip child) is itself rebuilt from its
+                               // one tip and its own rebuilt cherry (step s-2): a depth-2 chain
 
 // The device copy of the program packs a step into 8 ints (pack_program):
 //   w0 x | y<<16   w1 mx | my<<16   w2 mv | vslot<<16   w3 xslot | yslot<<16
@@ -703,7 +705,7 @@ __global__ void __launch_bounds__(MAXT) __attribute__((amdgpu_waves_per_eu(K == 
       const int x = r.st.x, y = r.st.y, fl = r.st.fl;                     \
       /* a rebuilt cherry (F_PREVREC) is the previous-step child: y when y is       \
          internal, else x -- its operand is not loaded */                           \
-      const bool rec_ = fl & F_PREVREC;                                             \
+      const bool rec_ = fl & (F_PREVREC | F_PREVREC2);  \
       const bool lx = ok && x < 0 && !(rec_ && y >= 0), ly = ok && y < 0 && !rec_;  \
       const bool lr = ok && (fl & F_VDEEP) && r.st.vd >= ndl;             \
       const int xs = r.st.xs, ys = r.st.ys, vd = r.st.vd;                 \
@@ -722,7 +724,22 @@ __global__ void __launch_bounds__(MAXT) __attribute__((amdgpu_waves_per_eu(K == 
         p_[k] = vmul(look(cst.mx, tipb(cst.x, k)), look(cst.my, tipb(cst.y, k)));                   \
       pvec_k<K>(mrec(cst.mv), p_, out);                                                             \
     } while (0)
-    #define RSTEP_V(s, cs, cn, XT, YT) do {                                                         \
+    /* depth 2: a_v of v (one tip child; the other, its previous step, a                  \
+       rebuilt cherry whose record is step s2), in the forward's operand order */         \
+    #define REBUILD2(vst, s2, out) do {                                                   \
+      const Step c2_ = ld_step(prog, s2);                                                 \
+      V4 ac_[K], p2_[K];                                                                  \
+      REBUILD(c2_, ac_);                                                                  \
+      if (vst.x >= 0) {                                                                   \
+      _Pragma("unroll")                                                                   \
+        for (int k = 0; k < K; ++k) p2_[k] = vmul(look(vst.mx, tipb(vst.x, k)), ac_[k]);  \
+      } else {                                                                            \
+      _Pragma("unroll")                                                                   \
+        for (int k = 0; k < K; ++k) p2_[k] = vmul(ac_[k], look(vst.my, tipb(vst.y, k)));  \
+      }                                                                                   \
+      pvec_k<K>(mrec(vst.mv), p2_, out);                                                  \
+    } while (0)
+    #define RSTEP_V(s, cs, cn, XT, YT) do {                                               \
       const Step& st = cs.st;                                                     \
       ensure_chunk(st);                                                           \
       const int fl = st.fl;                                                       \
@@ -750,6 +767,8 @@ __global__ void __launch_bounds__(MAXT) __attribute__((amdgpu_waves_per_eu(K == 
         }                                                                         \
       } else if (YT && (fl & F_PREVREC)) { /* x is the rebuilt previous-step child */  \
         REBUILD(cn.st, ax);                                                            \
+      } else if (YT && (fl & F_PREVREC2)) {                                            \
+        REBUILD2(cn.st, s - 2, ax);                                                    \
       } else {                                                                         \
       _Pragma("unroll")                                                                \
         for (int k = 0; k < K; ++k) ax[k] = cs.lx[k];                                  \
@@ -763,6 +782,8 @@ __global__ void __launch_bounds__(MAXT) __attribute__((amdgpu_waves_per_eu(K == 
         }                                                                         \
       } else if (fl & F_PREVREC) { /* y is the rebuilt previous-step child */  \
         REBUILD(cn.st, ay);                                                    \
+      } else if (fl & F_PREVREC2) {                                            \
+        REBUILD2(cn.st, s - 2, ay);                                            \
       } else {                                                                 \
       _Pragma("unroll")                                                        \
         for (int k = 0; k < K; ++k) ay[k] = cs.ly[k];                          \
@@ -1549,7 +1570,7 @@ int plan_chunks(phy_ctx* c) {
   }
   // recomputed cherries (F_NOSTORE / F_PREVREC), valid for this chunk plan
   c->nrec = 0;
-  for (int s = 0; s < c->nsteps; ++s) c->prog[(size_t)s * STEP_INTS + ST_FLAGS] &= ~(F_NOSTORE | F_PREVREC);
+  for (int s = 0; s < c->nsteps; ++s) c->prog[(size_t)s * STEP_INTS + ST_FLAGS] &= ~(F_NOSTORE | F_PREVREC | F_PREVREC2);
   if (c->recompute) {
     for (int s = 1; s < c->nsteps; ++s) {
       int* p = &c->prog[(size_t)s * STEP_INTS];
@@ -1560,6 +1581,16 @@ int plan_chunks(phy_ctx* c) {
       if (has_internal && cherry && p[ST_CHUNK] == q[ST_CHUNK]) {
         q[ST_FLAGS] |= F_NOSTORE;
         p[ST_FLAGS] |= F_PREVREC;
+        ++c->nrec;
+        continue;
+      }
+      // depth 2: the previous step has one tip child and rebuilds its other
+      // (previous-step) child, a cherry, from LDS
+      const bool one_tip = (q[ST_X] >= 0) != (q[ST_Y] >= 0);
+      if (s >= 2 && has_internal && one_tip && (q[ST_FLAGS] & F_PREVREC) && (q[ST_FLAGS] & F_MV) &&
+          q[ST_VSLOT] >= 0 && !(q[ST_FLAGS] & F_VDEEP) && p[ST_CHUNK] == q[ST_CHUNK]) {
+        q[ST_FLAGS] |= F_NOSTORE;
+        p[ST_FLAGS] |= F_PREVREC2;
         ++c->nrec;
       }
     }
