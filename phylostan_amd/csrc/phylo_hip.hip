@@ -268,6 +268,8 @@ struct SweepArgs {
   int S, P, Ppad, C, nsteps, nslots, ndeep, ndl, nblk, nmat, R, cap_m;  // ndl: deep entries in LDS
   int B, outlen, g_direct;  // g_direct: one workgroup per draw
   unsigned long long extra;  // tip masks of record vectors 4..R-1, 4 bits each
+  int fin;  // g_direct and the finalize fits in LDS: the sweep writes the whole output row
+  const double* blens;  // [draw][B] (fin)
 };
 
 // LDS carve (16-B aligned pieces), K columns per lane:
@@ -882,6 +884,11 @@ __global__ void __launch_bounds__(MAXT) __attribute__((amdgpu_waves_per_eu(K == 
     // back with agent-scope loads (past L1, same XCD's L2).  No device fence:
     // a release fence here would write back the whole L2 per workgroup.
     WAIT_VMCNT0();
+    // fin: the finalize runs here; its LDS (inner products [C][B], then the
+    // waves' scalar partials [C][8]) reuses the sweep's, once every wave is done
+    double* innerL = mats0;
+    double* scalL = mats0 + (size_t)C * a.B;
+    if (a.fin) __syncthreads();
     const double* Qd = a.eig + (size_t)draw * EIG_LEN + EIG_Q;
     double* gout = a.out + (size_t)draw * a.outlen + 1 + a.B + 2 * C + 4;
     double* inner_d = a.inner + (size_t)draw * C * a.B;
@@ -915,7 +922,46 @@ __global__ void __launch_bounds__(MAXT) __attribute__((amdgpu_waves_per_eu(K == 
           sv += __shfl_xor(sv, 2, 16);
           sv += __shfl_xor(sv, 1, 16);
           gout[((size_t)c * a.B + bb[u]) * 16 + e16] = g[u];
-          if (e16 == 0) inner_d[(size_t)c * a.B + bb[u]] = sv;
+          if (e16 == 0) {
+            inner_d[(size_t)c * a.B + bb[u]] = sv;
+            if (a.fin) innerL[(size_t)c * a.B + bb[u]] = sv;
+          }
+        }
+      }
+    }
+    if (a.fin) {
+      if (lane == 0) {
+        scalL[c * 8 + 0] = acc_ll;
+        scalL[c * 8 + 1] = acc_dps;
+        scalL[c * 8 + 2] = acc_f.x;
+        scalL[c * 8 + 3] = acc_f.y;
+        scalL[c * 8 + 4] = acc_f.z;
+        scalL[c * 8 + 5] = acc_f.w;
+      }
+      __syncthreads();
+      // finalize_kernel's sums, in its order (bitwise the same results)
+      const int B = a.B;
+      double* out = a.out + (size_t)draw * a.outlen;
+      const double* rs = mdl + 10;
+      const double* bl = a.blens + (size_t)draw * B;
+      for (int b = threadIdx.x; b < B; b += nthreads) {
+        double sacc = 0.0;
+        for (int cc = 0; cc < C; ++cc) sacc = fma(rs[cc], innerL[cc * B + b], sacc);
+        out[1 + b] = sacc;
+      }
+      for (int cc = threadIdx.x; cc < C; cc += nthreads) {
+        double sacc = 0.0;
+        for (int b = 0; b < B; ++b) sacc = fma(bl[b], innerL[cc * B + b], sacc);
+        out[1 + B + cc] = sacc;
+      }
+      if (threadIdx.x == 0) {
+        const double ll = scalL[0];
+        out[0] = isfinite(ll) ? ll : -INFINITY;
+        for (int cc = 0; cc < C; ++cc) out[1 + B + C + cc] = scalL[cc * 8 + 1];
+        for (int q = 0; q < 4; ++q) {
+          double t = 0.0;
+          for (int cc = 0; cc < C; ++cc) t += scalL[cc * 8 + 2 + q];
+          out[1 + B + 2 * C + q] = t;
         }
       }
     }
@@ -1256,6 +1302,7 @@ struct phy_ctx {
   bool deep_lds = false;       // current plan keeps the whole deep stack in LDS
   int ndl = 0;                 // deep entries in LDS (== ndeep when deep_lds)
   bool recompute = true;       // rebuild cherries in the reverse instead of storing them
+  bool fin_pref = true;        // finalize inside the sweep when one workgroup runs a draw (PHY_FIN=0: off)
   int nrec = 0;                // cherries recomputed under the current plan
   hipStream_t stream;
   std::vector<int> prog;  // host copy of the program (chunk fields per plan)
@@ -1623,11 +1670,14 @@ int launch(phy_ctx* ctx, int n, const double* d_blens, const double* d_model, do
   if ((size_t)gx * n > (size_t)ctx->wg_cap) return fail(PHY_ERANGE, "workgroup cap exceeded");
   const size_t lds = lds_bytes(ctx->S, C, ctx->R, ctx->cap_m, ctx->K, ctx->ndl);
   const int g_direct = (gx == 1) ? 1 : 0;
+  // finalize inside the sweep when its LDS holds [C][B] + [C][8] doubles past the tips
+  const int fin = (g_direct && ctx->fin_pref && ((size_t)C * B + 8 * C) * 8 <= lds - tip_lds_bytes(ctx->S, ctx->K))
+                      ? 1 : 0;
   SweepArgs sa{ctx->d_tips,  ctx->d_w,     ctx->d_pmat,  d_model,      ctx->d_scratch, ctx->d_dstk,
                ctx->d_gslot, ctx->d_sslot, d_site,       d_out,        ctx->d_mat_branch, ctx->d_eig,
                ctx->d_inner, ctx->S,       ctx->P,       ctx->Ppad,    C,              ctx->nsteps,
                ctx->nslots,  ctx->ndeep,   ctx->ndl,     ctx->nblk,    ctx->nmat,    ctx->R,         ctx->cap_m,
-               B,            phy_output_len(ctx), g_direct, ctx->extra};
+               B,            phy_output_len(ctx), g_direct, ctx->extra, fin, d_blens};
   hipEvent_t e0 = nullptr, e1 = nullptr;
   if (ctx->timing) {
     if (ctx->ev_used + 2 > (int)ctx->ev.size()) {
@@ -1665,8 +1715,10 @@ int launch(phy_ctx* ctx, int n, const double* d_blens, const double* d_model, do
     hipLaunchKernelGGL(gsum_kernel, dim3((C * B * 16 + 63) / 64, n), dim3(256), 0, st, fa);
     HIP_TRY(hipGetLastError());
   }
-  hipLaunchKernelGGL(finalize_kernel, dim3(n), dim3(256), ((size_t)C * B + 16) * sizeof(double), st, fa);
-  HIP_TRY(hipGetLastError());
+  if (!fin) {
+    hipLaunchKernelGGL(finalize_kernel, dim3(n), dim3(256), ((size_t)C * B + 16) * sizeof(double), st, fa);
+    HIP_TRY(hipGetLastError());
+  }
   return PHY_OK;
 }
 
@@ -1746,6 +1798,8 @@ int phy_create(int S, int P, int C, int rooted, int model, const uint8_t* tipcod
     c->deep_pref = dk ? std::max(0, std::min(2, atoi(dk))) : 0;
     const char* rk = getenv("PHY_RECOMPUTE");
     c->recompute = rk ? atoi(rk) != 0 : true;
+    const char* fk = getenv("PHY_FIN");
+    c->fin_pref = fk ? atoi(fk) != 0 : true;
   }
   hipError_t he = hipSetDevice(device);
   if (he != hipSuccess) {

@@ -247,3 +247,28 @@ def test_recomputed_cherries_bitwise(make):
     np.testing.assert_array_equal(res.site_ll, ref.site_ll)
     np.testing.assert_array_equal(res.dLdP, ref.dLdP)
     np.testing.assert_array_equal(res.grad_blens, ref.grad_blens)
+
+
+def test_finalize_inside_sweep_matches_kernel(monkeypatch):
+    """One workgroup per draw: the finalize folded into the sweep (default)
+    and the separate finalize kernel (PHY_FIN=0) give bit-identical rows."""
+    base = cases.fluA_case()
+    rng = np.random.default_rng(5)
+    n = 3
+    blens = base.blens[None, :] * rng.uniform(0.7, 1.3, (n, 1))
+    mv = np.repeat(base.model_vec()[None], n, axis=0)
+    eng = _engine(base, max_draws=n)
+    eng.set_tuning(n, 0, 0)  # one workgroup per draw
+    r1 = eng.evaluate_batch(blens, mv, site_ll=True)
+    monkeypatch.setenv("PHY_FIN", "0")
+    eng2 = _engine(base, max_draws=n)
+    eng2.set_tuning(n, 0, 0)
+    r2 = eng2.evaluate_batch(blens, mv, site_ll=True)
+    for a, b in zip(r1, r2):
+        assert a.loglik == b.loglik
+        np.testing.assert_array_equal(a.grad_blens, b.grad_blens)
+        np.testing.assert_array_equal(a.grad_rs, b.grad_rs)
+        np.testing.assert_array_equal(a.grad_ps, b.grad_ps)
+        np.testing.assert_array_equal(a.grad_freq_root, b.grad_freq_root)
+        np.testing.assert_array_equal(a.dLdP, b.dLdP)
+    check_case(base, eng2)
