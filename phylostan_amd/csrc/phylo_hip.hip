@@ -1088,59 +1088,76 @@ __global__ void __launch_bounds__(64) eig_kernel(PmatArgs a) {
 // order -- the four columns of P, then P t for each extra tip mask t (the
 // 0/1 sum of P's columns, in column order: bitwise what a mat-vec with the
 // 0/1 vector gives).
-__global__ void __launch_bounds__(256) pmat_kernel(PmatArgs a) {
+// One wave per 64 consecutive records of a draw (record idx = c*nmat + m,
+// contiguous in memory): each lane builds its record in LDS, then the wave
+// copies the 64 records out as one contiguous run (whole-line stores; a
+// record per lane straight to HBM would scatter every store instruction).
+constexpr int PMAT_WAVE_RECS = 64;
+__global__ void __launch_bounds__(64) pmat_kernel(PmatArgs a) {
   __shared__ double e[EIG_LEN];
+  extern __shared__ __attribute__((aligned(16))) double recl[];  // [64][R*4]
   const int draw = blockIdx.y;
   const int C = a.C, nmat = a.nmat;
-  if (threadIdx.x < EIG_LEN) e[threadIdx.x] = a.eig[(size_t)draw * EIG_LEN + threadIdx.x];
+  const int lane = threadIdx.x;
+  if (lane < EIG_LEN) e[lane] = a.eig[(size_t)draw * EIG_LEN + lane];
   __syncthreads();
-  const int idx = blockIdx.x * blockDim.x + threadIdx.x;
-  if (idx >= C * nmat) return;
-  const int c = idx / nmat, m = idx - c * nmat;
-  const int br = a.mat_branch[m];
-  double2* po = reinterpret_cast<double2*>(a.pmat + (((size_t)draw * C + c) * nmat + m) * a.R * 4);
-  double P[16];
-  {
-    const double* mdl = a.model + (size_t)draw * (10 + 2 * C);
-    const double t = a.blens[(size_t)draw * a.B + br] * mdl[10 + c];
-    if (a.kind == PHY_JC69) {  // generate_script.py:765-769
-      const double ex = exp(-t / 0.75);
-      const double off = 0.25 - 0.25 * ex, d = 0.25 + 0.75 * ex;
+  const int total = C * nmat;
+  const int idx0 = blockIdx.x * PMAT_WAVE_RECS;
+  const int nrec = min(PMAT_WAVE_RECS, total - idx0);
+  const int rlen = a.R * 4;  // doubles per record
+  const int idx = idx0 + lane;
+  if (lane < nrec) {
+    const int c = idx / nmat, m = idx - c * nmat;
+    const int br = a.mat_branch[m];
+    double2* po = reinterpret_cast<double2*>(recl + (size_t)lane * rlen);
+    double P[16];
+    {
+      const double* mdl = a.model + (size_t)draw * (10 + 2 * C);
+      const double t = a.blens[(size_t)draw * a.B + br] * mdl[10 + c];
+      if (a.kind == PHY_JC69) {  // generate_script.py:765-769
+        const double ex = exp(-t / 0.75);
+        const double off = 0.25 - 0.25 * ex, d = 0.25 + 0.75 * ex;
 #pragma unroll
-      for (int k = 0; k < 16; ++k) P[k] = (k % 5 == 0) ? d : off;
-    } else {  // m1 diag(exp(lam t)) m2   (:880)
-      double E[4];
+        for (int k = 0; k < 16; ++k) P[k] = (k % 5 == 0) ? d : off;
+      } else {  // m1 diag(exp(lam t)) m2   (:880)
+        double E[4];
 #pragma unroll
-      for (int l = 0; l < 4; ++l) E[l] = exp(e[EIG_LAM + l] * t);
+        for (int l = 0; l < 4; ++l) E[l] = exp(e[EIG_LAM + l] * t);
 #pragma unroll
-      for (int j = 0; j < 4; ++j)
+        for (int j = 0; j < 4; ++j)
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
-          double acc = 0.0;
+          for (int k = 0; k < 4; ++k) {
+            double acc = 0.0;
 #pragma unroll
-          for (int l = 0; l < 4; ++l) acc = fma(e[EIG_M1 + j * 4 + l] * E[l], e[EIG_M2 + l * 4 + k], acc);
-          P[j * 4 + k] = acc;
-        }
+            for (int l = 0; l < 4; ++l) acc = fma(e[EIG_M1 + j * 4 + l] * E[l], e[EIG_M2 + l * 4 + k], acc);
+            P[j * 4 + k] = acc;
+          }
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {  // column j
+      po[2 * j] = make_double2(P[j], P[4 + j]);
+      po[2 * j + 1] = make_double2(P[8 + j], P[12 + j]);
+    }
+    for (int v = 4; v < a.R; ++v) {
+      const unsigned t = (unsigned)(a.extra >> (4 * (v - 4))) & 15u;
+      double r[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        double acc = P[i * 4] * (double)(t & 1u);
+#pragma unroll
+        for (int j = 1; j < 4; ++j) acc = fma(P[i * 4 + j], (double)((t >> j) & 1u), acc);
+        r[i] = acc;
+      }
+      po[2 * v] = make_double2(r[0], r[1]);
+      po[2 * v + 1] = make_double2(r[2], r[3]);
     }
   }
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {  // column j
-    po[2 * j] = make_double2(P[j], P[4 + j]);
-    po[2 * j + 1] = make_double2(P[8 + j], P[12 + j]);
-  }
-  for (int v = 4; v < a.R; ++v) {
-    const unsigned t = (unsigned)(a.extra >> (4 * (v - 4))) & 15u;
-    double r[4];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      double acc = P[i * 4] * (double)(t & 1u);
-#pragma unroll
-      for (int j = 1; j < 4; ++j) acc = fma(P[i * 4 + j], (double)((t >> j) & 1u), acc);
-      r[i] = acc;
-    }
-    po[2 * v] = make_double2(r[0], r[1]);
-    po[2 * v + 1] = make_double2(r[2], r[3]);
-  }
+  __syncthreads();
+  const double2* src = reinterpret_cast<const double2*>(recl);
+  double2* dst = reinterpret_cast<double2*>(a.pmat + ((size_t)draw * total + idx0) * rlen);
+  const int n2 = nrec * rlen / 2;
+  for (int k = lane; k < n2; k += 64) dst[k] = src[k];
 }
 
 // ---------------------------------------------------------------------------
@@ -1661,7 +1678,8 @@ int launch(phy_ctx* ctx, int n, const double* d_blens, const double* d_model, do
                 ctx->R, ctx->extra};
     hipLaunchKernelGGL(eig_kernel, dim3((n + 63) / 64), dim3(64), 0, st, pa);
     HIP_TRY(hipGetLastError());
-    hipLaunchKernelGGL(pmat_kernel, dim3((C * ctx->nmat + 255) / 256, n), dim3(256), 0, st, pa);
+    hipLaunchKernelGGL(pmat_kernel, dim3((C * ctx->nmat + PMAT_WAVE_RECS - 1) / PMAT_WAVE_RECS, n), dim3(64),
+                       (size_t)PMAT_WAVE_RECS * ctx->R * 4 * sizeof(double), st, pa);
     HIP_TRY(hipGetLastError());
   }
   // persistent workgroups: the explicit budget, else exactly what is resident
