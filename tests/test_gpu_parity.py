@@ -272,3 +272,23 @@ def test_finalize_inside_sweep_matches_kernel(monkeypatch):
         np.testing.assert_array_equal(a.grad_freq_root, b.grad_freq_root)
         np.testing.assert_array_equal(a.dLdP, b.dLdP)
     check_case(base, eng2)
+
+
+@pytest.mark.parametrize("S,P,cat", [(400, 300, False), (300, 200, True)], ids=["random400", "caterpillar300"])
+def test_large_trees(S, P, cat):
+    """Hundreds of taxa: deep stacks, many LDS chunks, long rebuild chains."""
+    case = cases.random_case(61, S=S, P=P, C=4, model="GTR", caterpillar=cat)
+    eng = _engine(case)
+    plan = eng.lds_plan()
+    assert plan["n_chunks"] > 1
+    check_case(case, eng)
+
+
+def test_every_ambiguity_mask():
+    """All 15 non-empty 4-bit masks in the data: 15 record vectors per matrix."""
+    case = cases.random_case(62, S=20, P=400, C=3, model="HKY")
+    rng = np.random.default_rng(62)
+    codes = rng.integers(1, 16, size=case.tipcodes.shape).astype(np.uint8)
+    case = cases.Case("allmasks", codes, case.weights, case.peel0, True, "HKY", 3, case.blens, case.freqs,
+                      case.rates, case.rs, case.ps)
+    check_case(case)
