@@ -44,7 +44,7 @@ def parse():
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--workload", choices=["fluA", "synthetic"], default="fluA")
     ap.add_argument("--draws", type=int, default=None,
-                    help="parameter points per step (default: fluA 2048, synthetic 1)")
+                    help="parameter points per step (default: fluA 4096, synthetic 1)")
     ap.add_argument("--sites", type=int, default=1_000_000, help="synthetic: simulated sites")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="cpu_baseline sample length")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -148,7 +148,7 @@ def main():
 
     if args.workload == "fluA":
         prob = fluA_problem()
-        draws = args.draws or 2048
+        draws = args.draws or 4096
         shard_world, shard_rank = 1, 0  # replicas: every rank runs complete evaluations
     else:
         prob = synthetic_problem(args.sites)
