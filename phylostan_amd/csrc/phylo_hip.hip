@@ -76,6 +76,7 @@ enum {
   ST_M0,     // first matrix of that chunk
   ST_MN,     // matrices in that chunk
   ST_NODE,   // node id
+  ST_RD,     // rebuild depth of the previous-step child (F_PREVREC): 1 cherry, 2.. chain
 };
 constexpr int F_MV = 1;     // the step's branch has a matrix (else identity)
 constexpr int F_XDEEP = 2;  // both children internal: x's operand is on the deep stack
@@ -87,8 +88,7 @@ constexpr int F_VDEEP = 4;  // v is the x child of a both-internal parent
 // reverse loaded a step ahead).
 constexpr int F_NOSTORE = 8;   // this step's a_v is not written to scratch
 constexpr int F_PREVREC = 16;  // the child computed at the previous step is rebuilt, not loaded
-constexpr int F_PREVREC2 = 32; // ... and that child (one tip child) is itself rebuilt from its
-                               // one tip and its own rebuilt cherry (step s-2): a depth-2 chain
+constexpr int RD_MAX = 4;      // deepest rebuild chain: a cherry plus up to 3 one-tip nodes above it
 
 // The device copy of the program packs a step into 8 ints (pack_program):
 //   w0 x | y<<16   w1 mx | my<<16   w2 mv | vslot<<16   w3 xslot | yslot<<16
@@ -98,7 +98,7 @@ constexpr int F_PREVREC2 = 32; // ... and that child (one tip child) is itself r
 // a step ahead, replaces a chain of dependent scalar loads.
 constexpr int PSTEP = 8;
 struct Step {
-  int x, y, mx, my, mv, vs, fl, xs, ys, xd, vd, ch, m0, mn;
+  int x, y, mx, my, mv, vs, fl, xs, ys, xd, vd, ch, m0, mn, rd;
 };
 __device__ __forceinline__ int lo16(int w) { return (int)(short)(w & 0xFFFF); }
 __device__ __forceinline__ int hi16(int w) { return w >> 16; }
@@ -121,6 +121,7 @@ __device__ __forceinline__ Step ld_step(const int* __restrict__ prog, int s) {
   t.ch = lo16(b.y);
   t.m0 = hi16(b.y);
   t.mn = lo16(b.z);
+  t.rd = b.w;
   return t;
 }
 // Per-draw eigensystem record: P(t) = m1 diag(exp(lam t)) m2, plus Q.
@@ -707,7 +708,7 @@ __global__ void __launch_bounds__(MAXT) __attribute__((amdgpu_waves_per_eu(K == 
       const int x = r.st.x, y = r.st.y, fl = r.st.fl;                     \
       /* a rebuilt cherry (F_PREVREC) is the previous-step child: y when y is       \
          internal, else x -- its operand is not loaded */                           \
-      const bool rec_ = fl & (F_PREVREC | F_PREVREC2);  \
+      const bool rec_ = fl & F_PREVREC;                 \
       const bool lx = ok && x < 0 && !(rec_ && y >= 0), ly = ok && y < 0 && !rec_;  \
       const bool lr = ok && (fl & F_VDEEP) && r.st.vd >= ndl;             \
       const int xs = r.st.xs, ys = r.st.ys, vd = r.st.vd;                 \
@@ -726,20 +727,34 @@ __global__ void __launch_bounds__(MAXT) __attribute__((amdgpu_waves_per_eu(K == 
         p_[k] = vmul(look(cst.mx, tipb(cst.x, k)), look(cst.my, tipb(cst.y, k)));                   \
       pvec_k<K>(mrec(cst.mv), p_, out);                                                             \
     } while (0)
-    /* depth 2: a_v of v (one tip child; the other, its previous step, a                  \
-       rebuilt cherry whose record is step s2), in the forward's operand order */         \
-    #define REBUILD2(vst, s2, out) do {                                                   \
-      const Step c2_ = ld_step(prog, s2);                                                 \
-      V4 ac_[K], p2_[K];                                                                  \
-      REBUILD(c2_, ac_);                                                                  \
+    /* one level up a rebuilt chain: a_v of v (one tip child, the other the
+       rebuilt a_in), in the forward's operand order */
+    #define CHAIN_UP(vst, in, out) do {                                                   \
+      V4 pu_[K];                                                                          \
       if (vst.x >= 0) {                                                                   \
       _Pragma("unroll")                                                                   \
-        for (int k = 0; k < K; ++k) p2_[k] = vmul(look(vst.mx, tipb(vst.x, k)), ac_[k]);  \
+        for (int k = 0; k < K; ++k) pu_[k] = vmul(look(vst.mx, tipb(vst.x, k)), in[k]);   \
       } else {                                                                            \
       _Pragma("unroll")                                                                   \
-        for (int k = 0; k < K; ++k) p2_[k] = vmul(ac_[k], look(vst.my, tipb(vst.y, k)));  \
+        for (int k = 0; k < K; ++k) pu_[k] = vmul(in[k], look(vst.my, tipb(vst.y, k)));  \
       }                                                                                   \
-      pvec_k<K>(mrec(vst.mv), p2_, out);                                                  \
+      pvec_k<K>(mrec(vst.mv), pu_, out);                                                  \
+    } while (0)
+    /* the previous-step child of step s, rebuilt from the chain of depth d
+       below it: its cherry at step s-d, then one-tip nodes up to vst (s-1) */
+    #define REBUILDN(vst, s, d, out) do {                                                 \
+      if (d == 1) {                                                                       \
+        REBUILD(vst, out);                                                                \
+      } else {                                                                            \
+        const Step cb_ = ld_step(prog, s - d);                                            \
+        V4 acc_[K];                                                                       \
+        REBUILD(cb_, acc_);                                                               \
+        for (int j_ = d - 1; j_ >= 2; --j_) {                                             \
+          const Step v_ = ld_step(prog, s - j_);                                          \
+          CHAIN_UP(v_, acc_, acc_);                                                       \
+        }                                                                                 \
+        CHAIN_UP(vst, acc_, out);                                                         \
+      }                                                                                   \
     } while (0)
     #define RSTEP_V(s, cs, cn, XT, YT) do {                                               \
       const Step& st = cs.st;                                                     \
@@ -768,9 +783,7 @@ __global__ void __launch_bounds__(MAXT) __attribute__((amdgpu_waves_per_eu(K == 
           ax[k] = look(mx, bx[k]);                                                \
         }                                                                         \
       } else if (YT && (fl & F_PREVREC)) { /* x is the rebuilt previous-step child */  \
-        REBUILD(cn.st, ax);                                                            \
-      } else if (YT && (fl & F_PREVREC2)) {                                            \
-        REBUILD2(cn.st, s - 2, ax);                                                    \
+        REBUILDN(cn.st, s, st.rd, ax);                                                 \
       } else {                                                                         \
       _Pragma("unroll")                                                                \
         for (int k = 0; k < K; ++k) ax[k] = cs.lx[k];                                  \
@@ -783,9 +796,7 @@ __global__ void __launch_bounds__(MAXT) __attribute__((amdgpu_waves_per_eu(K == 
           ay[k] = look(my, by[k]);                                                \
         }                                                                         \
       } else if (fl & F_PREVREC) { /* y is the rebuilt previous-step child */  \
-        REBUILD(cn.st, ay);                                                    \
-      } else if (fl & F_PREVREC2) {                                            \
-        REBUILD2(cn.st, s - 2, ay);                                            \
+        REBUILDN(cn.st, s, st.rd, ay);                                         \
       } else {                                                                 \
       _Pragma("unroll")                                                        \
         for (int k = 0; k < K; ++k) ay[k] = cs.ly[k];                          \
@@ -1391,6 +1402,7 @@ std::vector<int> pack_program(const std::vector<int>& prog) {
                  ((unsigned)(p[ST_VDPOS] & 0xFF) << 16));
     q[5] = h(p[ST_CHUNK], p[ST_M0]);
     q[6] = h(p[ST_MN], p[ST_NODE]);
+    q[7] = p[ST_RD];
   }
   return out;
 }
@@ -1632,31 +1644,33 @@ int plan_chunks(phy_ctx* c) {
     const int m1 = (k < ch) ? c->prog[(size_t)first_step[k + 1] * STEP_INTS + ST_M0] : c->nmat;
     for (int s = first_step[k]; s < first_step[k + 1]; ++s) c->prog[(size_t)s * STEP_INTS + ST_MN] = m1 - m0;
   }
-  // recomputed cherries (F_NOSTORE / F_PREVREC), valid for this chunk plan
+  // rebuilt chains (F_NOSTORE / F_PREVREC / ST_RD), valid for this chunk plan:
+  // step s's previous-step child q is rebuilt at depth d when q is a cherry
+  // (d = 1) or has one tip child and itself rebuilds its previous-step child
+  // at depth d-1, and steps s-d..s share one LDS chunk
   c->nrec = 0;
-  for (int s = 0; s < c->nsteps; ++s) c->prog[(size_t)s * STEP_INTS + ST_FLAGS] &= ~(F_NOSTORE | F_PREVREC | F_PREVREC2);
+  for (int s = 0; s < c->nsteps; ++s) {
+    c->prog[(size_t)s * STEP_INTS + ST_FLAGS] &= ~(F_NOSTORE | F_PREVREC);
+    c->prog[(size_t)s * STEP_INTS + ST_RD] = 0;
+  }
   if (c->recompute) {
     for (int s = 1; s < c->nsteps; ++s) {
       int* p = &c->prog[(size_t)s * STEP_INTS];
       int* q = &c->prog[(size_t)(s - 1) * STEP_INTS];
       const bool has_internal = p[ST_X] < 0 || p[ST_Y] < 0;  // then step s-1 is its top child
-      const bool cherry = q[ST_X] >= 0 && q[ST_Y] >= 0 && (q[ST_FLAGS] & F_MV) && q[ST_VSLOT] >= 0 &&
-                          !(q[ST_FLAGS] & F_VDEEP);
-      if (has_internal && cherry && p[ST_CHUNK] == q[ST_CHUNK]) {
-        q[ST_FLAGS] |= F_NOSTORE;
-        p[ST_FLAGS] |= F_PREVREC;
-        ++c->nrec;
-        continue;
-      }
-      // depth 2: the previous step has one tip child and rebuilds its other
-      // (previous-step) child, a cherry, from LDS
-      const bool one_tip = (q[ST_X] >= 0) != (q[ST_Y] >= 0);
-      if (s >= 2 && has_internal && one_tip && (q[ST_FLAGS] & F_PREVREC) && (q[ST_FLAGS] & F_MV) &&
-          q[ST_VSLOT] >= 0 && !(q[ST_FLAGS] & F_VDEEP) && p[ST_CHUNK] == q[ST_CHUNK]) {
-        q[ST_FLAGS] |= F_NOSTORE;
-        p[ST_FLAGS] |= F_PREVREC2;
-        ++c->nrec;
-      }
+      const bool eligible = (q[ST_FLAGS] & F_MV) && q[ST_VSLOT] >= 0 && !(q[ST_FLAGS] & F_VDEEP);
+      if (!has_internal || !eligible) continue;
+      int d = 0;
+      if (q[ST_X] >= 0 && q[ST_Y] >= 0) d = 1;
+      else if ((q[ST_X] >= 0) != (q[ST_Y] >= 0) && q[ST_RD] > 0) d = q[ST_RD] + 1;
+      if (d == 0 || d > RD_MAX || s - d < 0) continue;
+      bool same = true;
+      for (int j = 1; j <= d; ++j) same = same && c->prog[(size_t)(s - j) * STEP_INTS + ST_CHUNK] == p[ST_CHUNK];
+      if (!same) continue;
+      q[ST_FLAGS] |= F_NOSTORE;
+      p[ST_FLAGS] |= F_PREVREC;
+      p[ST_RD] = d;
+      ++c->nrec;
     }
   }
   {
