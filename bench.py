@@ -106,9 +106,10 @@ def survey_bytes(S, P, C, draws):
     return P * (224 * C * (S - 2) + 3 * S + 16) * draws
 
 
-def cpu_baseline(prob, seconds):
+def cpu_baseline(prob, seconds, nthreads=1):
     """The C oracle (oracle/cpu_pruner.c, 'port') on the same workload,
-    single-threaded (Stan evaluates log_prob on one thread per chain)."""
+    single-threaded by default (Stan evaluates log_prob on one thread per
+    chain); nthreads > 1 runs its OpenMP loop over patterns."""
     from oracle import cpu
     from phylostan_amd import models
     kind = models.MODEL_IDS[prob["model"]]
@@ -119,14 +120,16 @@ def cpu_baseline(prob, seconds):
     out = None
     while True:
         out, _ = cpu.evaluate(prob["tipcodes"], prob["weights"], prob["peel0"], prob["rooted"], kind, mv,
-                              prob["blens"], prob["C"], nthreads=1)
+                              prob["blens"], prob["C"], nthreads=nthreads)
         n += 1
         el = time.perf_counter() - t0
         if el >= seconds:
             break
-    return dict(value=n / el, unit="evals/s", cores=1, kind="port",
+    return dict(value=n / el, unit="evals/s", cores=nthreads, kind="port",
                 sample="%d full log-lik+grad evaluations of the %d-taxon x %d-pattern workload in %.1f s, "
-                       "1 thread (oracle/cpu_pruner.c, gcc -O2)" % (n, S, P, el)), out
+                       "%d thread%s (oracle/cpu_pruner.c, gcc -O2%s)"
+                       % (n, S, P, el, nthreads, "" if nthreads == 1 else "s",
+                          "" if nthreads == 1 else ", OpenMP over patterns")), out
 
 
 def main():
@@ -253,11 +256,15 @@ def main():
         except (OSError, ValueError):
             traffic = None
 
-    cpu = None
+    cpu = cpu_mt = None
     if rank == 0 and not args.no_cpu_baseline:
         cpu, cpu_out = cpu_baseline(prob, args.cpu_seconds)
         # the cpu sample evaluates draw-0's nominal parameters; report its loglik
         cpu["loglik"] = float(cpu_out[0])
+        # the same port on all the host threads this job may use (reported beside it)
+        nt = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)
+        if nt > 1:
+            cpu_mt, _ = cpu_baseline(prob, max(2.0, args.cpu_seconds / 2), nthreads=nt)
 
     if rank == 0:
         rec = {
@@ -290,6 +297,7 @@ def main():
                 "survey_model_bytes_per_launch": survey_bytes(S, P_local, C, draws),
             },
             "cpu_baseline": cpu,
+            "cpu_baseline_all_threads": cpu_mt,
             "loglik_draw0": ll_last,
             "single_eval": single,
             "program": info,
