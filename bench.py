@@ -42,7 +42,7 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=20)
-    ap.add_argument("--workload", choices=["fluA", "synthetic"], default="fluA")
+    ap.add_argument("--workload", choices=["fluA", "synthetic", "HCV", "DS1"], default="fluA")
     ap.add_argument("--draws", type=int, default=None,
                     help="parameter points per step (default: fluA 4096, synthetic 1)")
     ap.add_argument("--sites", type=int, default=1_000_000, help="synthetic: simulated sites")
@@ -69,6 +69,40 @@ def fluA_problem():
     c = cases.fluA_case()
     return dict(tipcodes=c.tipcodes, weights=c.weights, peel0=c.peel0, rooted=True, model="HKY",
                 C=4, blens=c.blens, freqs=c.freqs, kappa=5.58, rates=c.rates, rs=c.rs, ps=c.ps)
+
+
+def hcv_problem():
+    """BASELINE config 3: examples/HCV, GTR+W4 at rates (1,2,1,1,2,1)/8, pi = 1/4,
+    alpha 0.5, clock rate 7.9e-4 on the input-tree heights (SConstruct:218)."""
+    from tests import cases
+    c = cases.hcv_case()
+    return dict(tipcodes=c.tipcodes, weights=c.weights, peel0=c.peel0, rooted=True, model="GTR",
+                C=4, blens=c.blens, freqs=c.freqs, kappa=None, rates=c.rates, rs=c.rs, ps=c.ps)
+
+
+def ds1_problem():
+    """BASELINE config 1: examples/DS1 tree 0, JC69 unrooted (root branch
+    merged), blens ~ Exp(10) seed 0 -- the reference runs it on the CPU only."""
+    from tests import cases
+    c = cases.ds1_case()
+    return dict(tipcodes=c.tipcodes, weights=c.weights, peel0=c.peel0, rooted=False, model="JC69",
+                C=1, blens=c.blens, freqs=c.freqs, kappa=None, rates=c.rates, rs=np.asarray(c.rs),
+                ps=np.asarray(c.ps))
+
+
+BATCHED = {"fluA": fluA_problem, "HCV": hcv_problem, "DS1": ds1_problem}
+METRIC = {
+    "fluA": "log-lik+grad evals/sec (HKY+W4, 69 taxa) at 1/2/4/8 MI355X; HBM-BW fraction",
+    "HCV": "log-lik+grad evals/sec (GTR+W4, 63 taxa, HCV)",
+    "DS1": "log-lik+grad evals/sec (JC69 unrooted, 27 taxa, DS1)",
+    "synthetic": "log-lik+grad evals/sec (GTR+W4, 128 taxa x 1M sites)",
+}
+DATA = {
+    "fluA": "fluA alignment patterns + input-tree heights (tests/golden fixture of examples/fluA)",
+    "HCV": "HCV alignment patterns + input-tree heights (tests/golden fixture of examples/HCV)",
+    "DS1": "DS1 alignment patterns + tree 0, branch lengths ~ Exp(10) seed 0 (tests/golden fixture)",
+    "synthetic": "synthetic (Kingman 128 taxa, simulated GTR+W4 sites, seed 0)",
+}
 
 
 def synthetic_problem(sites):
@@ -149,8 +183,9 @@ def main():
     from phylostan_amd import models
     from phylostan_amd.distributed import ShardedLikelihood
 
-    if args.workload == "fluA":
-        prob = fluA_problem()
+    batched = args.workload in BATCHED
+    if batched:
+        prob = BATCHED[args.workload]()
         draws = args.draws or 4096
         shard_world, shard_rank = 1, 0  # replicas: every rank runs complete evaluations
     else:
@@ -220,7 +255,7 @@ def main():
         kern_avg_ms = kern_ms / max(nlaunch, 1)
     ll_last = float(d_out[0, 0].item())
 
-    if args.workload == "fluA":
+    if batched:
         total_evals = world * draws * args.steps
     else:
         total_evals = draws * args.steps
@@ -268,8 +303,7 @@ def main():
 
     if rank == 0:
         rec = {
-            "metric": "log-lik+grad evals/sec (HKY+W4, 69 taxa) at 1/2/4/8 MI355X; HBM-BW fraction"
-            if args.workload == "fluA" else "log-lik+grad evals/sec (GTR+W4, 128 taxa x 1M sites)",
+            "metric": METRIC[args.workload],
             "value": value,
             "unit": "evals/s",
             "n_gpus": world,
@@ -277,17 +311,18 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": 1e3 * elapsed / args.steps,
             "higher_is_better": True,
-            "scaling": "weak" if args.workload == "fluA" else "strong",
+            "scaling": "weak" if batched else "strong",
             "vs_baseline": None,
             "dtype": "f64",
-            "data": "fluA alignment patterns + input-tree heights (tests/golden fixture of examples/fluA)"
-            if args.workload == "fluA" else "synthetic (Kingman 128 taxa, simulated GTR+W4 sites, seed 0)",
+            "data": DATA[args.workload],
             "config": {
-                "workload": "fluA HKY+W4 strict clock, %d parameter draws per step" % draws
-                if args.workload == "fluA" else "synthetic 128 x %d sites GTR+W4, pattern-sharded" % args.sites,
+                "workload": {"fluA": "fluA HKY+W4 strict clock, %d parameter draws per step" % draws,
+                             "HCV": "HCV GTR+W4 strict clock, %d parameter draws per step" % draws,
+                             "DS1": "DS1 JC69 unrooted, %d parameter draws per step" % draws}.get(
+                    args.workload, "synthetic 128 x %d sites GTR+W4, pattern-sharded" % args.sites),
                 "taxa": S, "patterns": P, "patterns_per_rank": P_local, "categories": C,
                 "branches": B, "draws_per_step": draws,
-                "parallelism": ("replicas%d" % world) if args.workload == "fluA" else ("patterns%d" % world),
+                "parallelism": ("replicas%d" % world) if batched else ("patterns%d" % world),
             },
             "roofline": {
                 "bound": "hbm", "achieved": achieved, "peak": PEAK_HBM_GBPS, "unit": "GB/s",
