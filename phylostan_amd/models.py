@@ -146,6 +146,65 @@ def q_param_gradients(dLdP, blens, rs, freqs, rates, grad_freq_root=None):
     return grad_rates, grad_freqs
 
 
+def q_param_gradients_batch(dLdP, blens, rs, freqs, rates, grad_freq_root=None):
+    """``q_param_gradients`` for n draws at once (dLdP [n, C, B, 4, 4], blens
+    [n, B], rs [n, C], freqs [n, 4], rates [n, 6]) -> (grad_rates [n, 6],
+    grad_freqs [n, 4]).  Same algebra, vectorised: with M the eigenbasis
+    contraction of G and W = V^-T M V^T, each parameter's gradient is
+    (sum(dQt * W) - ds * sum(Q * W)) / s with dQt's few nonzeros written out."""
+    f = np.asarray(freqs, np.float64)
+    rt = np.asarray(rates, np.float64)
+    n = f.shape[0]
+    R = np.zeros((n, 4, 4))
+    for k, (i, j) in enumerate(GTR_PAIRS):
+        R[:, i, j] = R[:, j, i] = rt[:, k]
+    Qt = R * f[:, None, :]
+    idx = np.arange(4)
+    Qt[:, idx, idx] = 0.0
+    Qt[:, idx, idx] = -Qt.sum(axis=2)
+    s = -np.einsum("nii,ni->n", Qt, f)
+    Q = Qt / s[:, None, None]
+    sq = np.sqrt(f)
+    A = sq[:, :, None] * Q / sq[:, None, :]
+    A = 0.5 * (A + np.swapaxes(A, 1, 2))
+    lam, U = np.linalg.eigh(A)
+    V = U / sq[:, :, None]
+    Vinv = np.swapaxes(U, 1, 2) * sq[:, None, :]
+    t = np.asarray(rs, np.float64)[:, :, None] * np.asarray(blens, np.float64)[:, None, :]  # [n, C, B]
+    VT = np.swapaxes(V, 1, 2)[:, None, None]
+    VinvT = np.swapaxes(Vinv, 1, 2)[:, None, None]
+    H = np.matmul(np.matmul(VT, np.asarray(dLdP, np.float64)), VinvT)  # V^T G V^-T per (c, b)
+    tt = t[..., None, None]
+    lk = lam[:, None, None, :, None]
+    ll = lam[:, None, None, None, :]
+    ek = np.exp(lk * tt)
+    el = np.exp(ll * tt)
+    d = lk - ll
+    same = np.abs(d) < 1e-12 * np.maximum(1.0, np.abs(lk))
+    with np.errstate(divide="ignore", invalid="ignore"):
+        phi = np.where(same, tt * ek, (ek - el) / np.where(same, 1.0, d))
+    M = (H * phi).sum(axis=(1, 2))  # [n, 4, 4]
+    W = np.matmul(np.matmul(np.swapaxes(Vinv, 1, 2), M), np.swapaxes(V, 1, 2))  # sum(dQ*W) = sum((Vinv dQ V)*M)
+    qw = (Q * W).sum(axis=(1, 2))
+    grad_rates = np.empty((n, 6))
+    for k, (i, j) in enumerate(GTR_PAIRS):
+        dq = f[:, j] * W[:, i, j] + f[:, i] * W[:, j, i] - f[:, j] * W[:, i, i] - f[:, i] * W[:, j, j]
+        ds = 2.0 * f[:, i] * f[:, j]
+        grad_rates[:, k] = (dq - ds * qw) / s
+    grad_freqs = np.empty((n, 4))
+    for m in range(4):
+        dq = np.zeros(n)
+        ds = np.zeros(n)
+        for j in range(4):
+            if j != m:
+                dq += R[:, j, m] * (W[:, j, m] - W[:, j, j])
+                ds += 2.0 * R[:, m, j] * f[:, j]
+        grad_freqs[:, m] = (dq - ds * qw) / s
+    if grad_freq_root is not None:
+        grad_freqs = grad_freqs + np.asarray(grad_freq_root, np.float64)
+    return grad_rates, grad_freqs
+
+
 def kappa_gradient(grad_rates):
     """HKY: kappa enters exchangeabilities AG and CT."""
     return float(grad_rates[1] + grad_rates[4])

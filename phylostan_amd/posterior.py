@@ -524,16 +524,16 @@ class Posterior:
         g_rs = np.stack([r.grad_rs if r is not None else zc for r in res])
         g_ps = np.stack([r.grad_ps if r is not None else zc for r in res])
         if sp.model != "JC69":
-            for d in range(n):
-                if bad[d]:
-                    continue
-                gr, gf = models.q_param_gradients(res[d].dLdP, blens[d], rs[d], freqs[d], R[d],
-                                                  res[d].grad_freq_root)
-                gx["freqs"][d] += gf
+            good = np.nonzero(~bad)[0]
+            if len(good):
+                gr, gf = models.q_param_gradients_batch(
+                    np.stack([res[d].dLdP for d in good]), blens[good], rs[good], freqs[good], R[good],
+                    np.stack([res[d].grad_freq_root for d in good]))
+                gx["freqs"][good] += gf
                 if sp.model == "GTR":
-                    gx["rates"][d] += gr
+                    gx["rates"][good] += gr
                 else:
-                    gx["kappa"][d] += models.kappa_gradient(gr)
+                    gx["kappa"][good] += gr[:, 1] + gr[:, 4]  # kappa_gradient: AG and CT
         self._site_rates_backward(vals, g_rs, g_ps, gx, rs, ps)
         if self.clock:
             gspan = g_bl * mult
