@@ -174,3 +174,20 @@ def test_linearity_over_pattern_shards():
     b = npr.prune(case.tipcodes[:, 37:], case.weights[37:], case.peel0, True, P, case.freqs, case.ps)
     assert abs(a["loglik"] + b["loglik"] - full["loglik"]) < 1e-9
     np.testing.assert_allclose(a["dLdP"] + b["dLdP"], full["dLdP"], rtol=1e-12, atol=1e-12)
+
+
+def test_q_param_gradients_batch_matches_per_draw():
+    """The vectorised chain rule (posterior's path) equals the per-draw one."""
+    rng = np.random.default_rng(7)
+    n, C, B = 3, 4, 15
+    G = rng.normal(size=(n, C, B, 4, 4))
+    bl = rng.uniform(0.01, 0.5, (n, B))
+    rs = rng.uniform(0.2, 2.0, (n, C))
+    f = rng.dirichlet(np.full(4, 3.0), n)
+    rt = rng.uniform(0.5, 3.0, (n, 6))
+    fr = rng.normal(size=(n, 4))
+    gr, gf = models.q_param_gradients_batch(G, bl, rs, f, rt, fr)
+    for d in range(n):
+        a, b = models.q_param_gradients(G[d], bl[d], rs[d], f[d], rt[d], fr[d])
+        np.testing.assert_allclose(gr[d], a, rtol=1e-12, atol=1e-12 * np.max(np.abs(a)))
+        np.testing.assert_allclose(gf[d], b, rtol=1e-12, atol=1e-12 * np.max(np.abs(b)))
