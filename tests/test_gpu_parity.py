@@ -292,3 +292,12 @@ def test_every_ambiguity_mask():
     case = cases.Case("allmasks", codes, case.weights, case.peel0, True, "HKY", 3, case.blens, case.freqs,
                       case.rates, case.rs, case.ps)
     check_case(case)
+
+
+@pytest.mark.parametrize("C", [9, 16])
+def test_many_categories(C):
+    """C > 8 rate categories: one column per lane, C waves per workgroup."""
+    case = cases.random_case(63, S=24, P=150, C=C, model="GTR")
+    eng = _engine(case)
+    assert eng.lds_plan()["cols"] == 1
+    check_case(case, eng)
