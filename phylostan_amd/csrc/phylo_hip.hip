@@ -53,10 +53,10 @@ namespace {
 
 constexpr int WAVE = 64;
 #ifndef PHY_ABLATE
-#define PHY_ABLATE 0  // diagnostic builds only: 2 = no reverse pass
-#endif
-#ifndef PHY_FWD_COND
-#define PHY_FWD_COND 0
+// Diagnostic builds only (timing of the sweep's pieces; results are wrong by
+// construction): 2 = no reverse pass, 4 = no per-draw epilogue, 8 = no
+// moved-partial stores.
+#define PHY_ABLATE 0
 #endif
 // Program step (STEP_INTS ints, host-built by build_program).
 constexpr int STEP_INTS = 16;
