@@ -174,15 +174,16 @@ def q_param_gradients_batch(dLdP, blens, rs, freqs, rates, grad_freq_root=None):
     VT = np.swapaxes(V, 1, 2)[:, None, None]
     VinvT = np.swapaxes(Vinv, 1, 2)[:, None, None]
     H = np.matmul(np.matmul(VT, np.asarray(dLdP, np.float64)), VinvT)  # V^T G V^-T per (c, b)
-    tt = t[..., None, None]
+    # Phi[k, l] = (e^{lam_k t} - e^{lam_l t}) / (lam_k - lam_l), t e^{lam_k t} on ties;
+    # the exponentials depend on k only, so they are taken once per (c, b, k)
+    E = np.exp(lam[:, None, None, :] * t[..., None])  # [n, C, B, 4]
+    ek = E[..., :, None]
+    el = E[..., None, :]
     lk = lam[:, None, None, :, None]
-    ll = lam[:, None, None, None, :]
-    ek = np.exp(lk * tt)
-    el = np.exp(ll * tt)
-    d = lk - ll
+    d = lk - lam[:, None, None, None, :]
     same = np.abs(d) < 1e-12 * np.maximum(1.0, np.abs(lk))
     with np.errstate(divide="ignore", invalid="ignore"):
-        phi = np.where(same, tt * ek, (ek - el) / np.where(same, 1.0, d))
+        phi = np.where(same, t[..., None, None] * ek, (ek - el) / np.where(same, 1.0, d))
     M = (H * phi).sum(axis=(1, 2))  # [n, 4, 4]
     W = np.matmul(np.matmul(np.swapaxes(Vinv, 1, 2), M), np.swapaxes(V, 1, 2))  # sum(dQ*W) = sum((Vinv dQ V)*M)
     qw = (Q * W).sum(axis=(1, 2))
