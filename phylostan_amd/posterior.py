@@ -433,7 +433,9 @@ class Posterior:
             h = self._heights(vals, n)
             span = self._span(h)
             mult, subs = self._multiplier(vals, n)
-            blens = span * mult
+            # extreme draws may overflow here; they are rejected just below
+            with np.errstate(over="ignore", invalid="ignore"):
+                blens = span * mult
         else:
             blens = vals["blens"]
 
