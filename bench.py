@@ -44,7 +44,7 @@ def parse():
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--workload", choices=["fluA", "synthetic", "HCV", "DS1"], default="fluA")
     ap.add_argument("--draws", type=int, default=None,
-                    help="parameter points per step (default: fluA 4096, synthetic 1)")
+                    help="parameter points per step (default: fluA/HCV/DS1 8192, synthetic 1)")
     ap.add_argument("--sites", type=int, default=1_000_000, help="synthetic: simulated sites")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="cpu_baseline sample length")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -186,7 +186,7 @@ def main():
     batched = args.workload in BATCHED
     if batched:
         prob = BATCHED[args.workload]()
-        draws = args.draws or 4096
+        draws = args.draws or 8192
         shard_world, shard_rank = 1, 0  # replicas: every rank runs complete evaluations
     else:
         prob = synthetic_problem(args.sites)

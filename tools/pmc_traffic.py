@@ -48,7 +48,7 @@ def main():
     ap.add_argument("--scratch", default=os.path.join(ROOT, "gpurun_out", "pmc"))
     args = ap.parse_args()
     from bench import kernel_source_hash
-    draws = args.draws or (4096 if args.workload == "fluA" else 1)
+    draws = args.draws or (8192 if args.workload == "fluA" else 1)
     bench_args = ["--workload", args.workload, "--draws", str(draws), "--steps", "3", "--warmup", "1",
                   "--no-cpu-baseline"]
     fetch, nf = run_pass("FETCH_SIZE", os.path.join(args.scratch, args.workload + "_fetch"), bench_args)
