@@ -54,6 +54,9 @@ def parse():
     ap.add_argument("--cols", type=int, default=0, help="pattern columns per lane (0 = automatic)")
     ap.add_argument("--lds-budget", type=int, default=0)
     ap.add_argument("--json-out", default=None)
+    ap.add_argument("--dry-run", action="store_true",
+                    help="launcher check only: ranks join a gloo group on the CPU, all-reduce their rank "
+                         "ids and exit (no GPU, no evaluation)")
     return ap.parse_args()
 
 
@@ -140,8 +143,39 @@ def survey_bytes(S, P, C, draws):
     return P * (224 * C * (S - 2) + 3 * S + 16) * draws
 
 
-def cpu_baseline(prob, seconds, nthreads=1):
-    """The C oracle (oracle/cpu_pruner.c, 'port') on the same workload,
+def host_cpu_info():
+    """CPU model, nproc, and the host threads this job may use: the CPUs in
+    its affinity mask, capped by a cgroup CPU quota when one is set (the GPU
+    box gives each one-GPU job a share of a larger machine)."""
+    model = None
+    try:
+        with open("/proc/cpuinfo") as fp:
+            for line in fp:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    nproc = os.cpu_count() or 1
+    try:
+        usable = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        usable = nproc
+    quota = None
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as fp:
+            q, per = fp.read().split()[:2]
+            if q != "max":
+                quota = max(1, int(int(q) // int(per)))
+    except (OSError, ValueError):
+        pass
+    threads = min(usable, quota) if quota else usable
+    return dict(model=model, nproc=nproc, affinity=usable, cgroup_quota_cpus=quota, threads=threads)
+
+
+def cpu_baseline(prob, seconds, nthreads=1, info=None):
+    """The C oracle (oracle/cpu_pruner.c, 'port') on the same workload at the
+    nominal parameter point (= the GPU's draw 0 of parameter set 0),
     single-threaded by default (Stan evaluates log_prob on one thread per
     chain); nthreads > 1 runs its OpenMP loop over patterns."""
     from oracle import cpu
@@ -159,28 +193,87 @@ def cpu_baseline(prob, seconds, nthreads=1):
         el = time.perf_counter() - t0
         if el >= seconds:
             break
-    return dict(value=n / el, unit="evals/s", cores=nthreads, kind="port",
-                sample="%d full log-lik+grad evaluations of the %d-taxon x %d-pattern workload in %.1f s, "
-                       "%d thread%s (oracle/cpu_pruner.c, gcc -O2%s)"
-                       % (n, S, P, el, nthreads, "" if nthreads == 1 else "s",
-                          "" if nthreads == 1 else ", OpenMP over patterns")), out
+    rec = dict(value=n / el, unit="evals/s", cores=nthreads, kind="port",
+               sample="%d full log-lik+grad evaluations of the %d-taxon x %d-pattern workload in %.1f s, "
+                      "%d thread%s (oracle/cpu_pruner.c, gcc -O2%s)"
+                      % (n, S, P, el, nthreads, "" if nthreads == 1 else "s",
+                         "" if nthreads == 1 else ", OpenMP over patterns"))
+    if info:
+        rec.update(cpu_model=info["model"], nproc=info["nproc"], affinity_cpus=info["affinity"],
+                   cgroup_quota_cpus=info["cgroup_quota_cpus"])
+    return rec, out
+
+
+def spawn_ranks(args):
+    """``python bench.py --gpus N`` without a launcher: start N rank processes
+    through torch.distributed.run (one per GPU) before anything touches HIP,
+    and exit with the launcher's code."""
+    import socket
+    import subprocess
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        port = so.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(args.gpus),
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    return subprocess.call(cmd, env=env)
+
+
+def parameter_sets(prob, nuniq, draws, B, C, rng):
+    """Distinct parameter points for every step.  Draw 0 of set 0 is the
+    nominal point the CPU baseline evaluates (the cross-check); every other
+    draw scales the branch lengths by U(0.8, 1.25) and kappa (HKY) or the
+    exchangeabilities (GTR/JC69) by random factors."""
+    from phylostan_amd import models
+    blens = np.empty((nuniq, draws, B))
+    mvs = np.empty((nuniq, draws, 10 + 2 * C))
+    for k in range(nuniq):
+        scale = rng.uniform(0.8, 1.25, (draws, 1))
+        if k == 0:
+            scale[0] = 1.0
+        blens[k] = prob["blens"][None, :] * scale
+        for d in range(draws):
+            nominal = k == 0 and d == 0
+            if prob["kappa"] is not None:
+                rates = models.hky_exchangeabilities(prob["kappa"] * (1.0 if nominal else rng.uniform(0.8, 1.25)))
+            else:
+                rates = prob["rates"] * (1.0 if nominal else rng.uniform(0.9, 1.1, 6))
+            mvs[k, d] = models.model_vector(prob["freqs"], rates, prob["rs"], prob["ps"])
+    return blens, mvs
 
 
 def main():
     args = parse()
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is None and args.gpus > 1:
+        sys.exit(spawn_ranks(args))
+    world = int(env_world or "1")
+    if world != args.gpus:
+        raise SystemExit("bench.py: --gpus %d but WORLD_SIZE=%d (one rank per GPU)" % (args.gpus, world))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
     import torch
     import torch.distributed as dist
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.dry_run:
+        total = rank
+        if world > 1:
+            dist.init_process_group("gloo")
+            t = torch.tensor([rank], dtype=torch.int64)
+            dist.all_reduce(t)
+            total = int(t.item())
+            dist.destroy_process_group()
+        if rank == 0:
+            print(json.dumps({"dry_run": True, "n_gpus": world, "sum_of_ranks": total}), flush=True)
+        return
+
     if world > 1:
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
 
-    from phylostan_amd import models
     from phylostan_amd.distributed import ShardedLikelihood
 
     batched = args.workload in BATCHED
@@ -209,17 +302,7 @@ def main():
     rng = np.random.default_rng(1234 + rank)
     nsets = args.warmup + args.steps
     nuniq = min(nsets, 16)
-    blens = np.empty((nuniq, draws, B))
-    mvs = np.empty((nuniq, draws, 10 + 2 * C))
-    for k in range(nuniq):
-        scale = rng.uniform(0.8, 1.25, (draws, 1))
-        blens[k] = prob["blens"][None, :] * scale
-        for d in range(draws):
-            if prob["kappa"] is not None:
-                rates = models.hky_exchangeabilities(prob["kappa"] * rng.uniform(0.8, 1.25))
-            else:
-                rates = prob["rates"] * rng.uniform(0.9, 1.1, 6)
-            mvs[k, d] = models.model_vector(prob["freqs"], rates, prob["rs"], prob["ps"])
+    blens, mvs = parameter_sets(prob, nuniq, draws, B, C, rng)
     d_blens = torch.tensor(blens, device=dev, dtype=torch.float64)
     d_model = torch.tensor(mvs, device=dev, dtype=torch.float64)
     d_out = torch.zeros((draws, eng.outlen), device=dev, dtype=torch.float64)
@@ -253,13 +336,42 @@ def main():
         kern_avg_ms = float(km.item())
     else:
         kern_avg_ms = kern_ms / max(nlaunch, 1)
-    ll_last = float(d_out[0, 0].item())
 
     if batched:
         total_evals = world * draws * args.steps
     else:
         total_evals = draws * args.steps
     value = total_evals / elapsed
+
+    # host-inclusive: the same steps, each followed by the D2H copy of every
+    # draw's full output row (what a host sampler consumes) into pinned memory
+    h_out = torch.empty((draws, eng.outlen), dtype=torch.float64, pin_memory=True)
+    nh = max(1, min(args.steps, 20))
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    ta = time.perf_counter()
+    for k in range(nh):
+        step(k)
+        h_out.copy_(d_out, non_blocking=True)
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    tb = time.perf_counter()
+    host_el = tb - ta
+    if world > 1:
+        t = torch.tensor([host_el], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        host_el = float(t.item())
+    host_inclusive = dict(value=(total_evals / args.steps) * nh / host_el, unit="evals/s", steps=nh,
+                          bytes_to_host_per_eval=8 * eng.outlen,
+                          note="each step followed by the D2H copy of every draw's output row "
+                               "(log-lik, gradients, dL/dP) into pinned host memory")
+
+    # cross-check: parameter set 0, draw 0 is the nominal point
+    step(0)
+    torch.cuda.synchronize(dev)
+    ll_nominal = float(d_out[0, 0].item())
 
     single = None
     if args.single_eval and rank == 0:
@@ -291,15 +403,17 @@ def main():
         except (OSError, ValueError):
             traffic = None
 
-    cpu = cpu_mt = None
+    cpu = cpu_mt = check = None
     if rank == 0 and not args.no_cpu_baseline:
-        cpu, cpu_out = cpu_baseline(prob, args.cpu_seconds)
-        # the cpu sample evaluates draw-0's nominal parameters; report its loglik
-        cpu["loglik"] = float(cpu_out[0])
-        # the same port on all the host threads this job may use (reported beside it)
-        nt = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)
-        if nt > 1:
-            cpu_mt, _ = cpu_baseline(prob, max(2.0, args.cpu_seconds / 2), nthreads=nt)
+        hinfo = host_cpu_info()
+        cpu, cpu_out = cpu_baseline(prob, args.cpu_seconds, info=hinfo)
+        # the same port on every host thread this job may use (reported beside it)
+        if hinfo["threads"] > 1:
+            cpu_mt, _ = cpu_baseline(prob, max(2.0, args.cpu_seconds / 2), nthreads=hinfo["threads"], info=hinfo)
+        if shard_world == 1:
+            ref = float(cpu_out[0])
+            rel = abs(ll_nominal - ref) / max(abs(ref), 1e-300)
+            check = dict(gpu_loglik_nominal=ll_nominal, cpu_loglik_nominal=ref, rel_err=rel, ok=rel <= 1e-10)
 
     if rank == 0:
         rec = {
@@ -333,7 +447,8 @@ def main():
             },
             "cpu_baseline": cpu,
             "cpu_baseline_all_threads": cpu_mt,
-            "loglik_draw0": ll_last,
+            "host_inclusive": host_inclusive,
+            "nominal_check": check,
             "single_eval": single,
             "program": info,
             "kernel_source": kernel_source_hash(),
@@ -343,6 +458,9 @@ def main():
         if args.json_out:
             with open(args.json_out, "w") as fp:
                 fp.write(line + "\n")
+        if check is not None and not check["ok"]:
+            print("bench.py: GPU nominal log-lik disagrees with the CPU port", file=sys.stderr)
+            sys.exit(3)
     if world > 1:
         dist.destroy_process_group()
 

@@ -1,9 +1,14 @@
-"""Mean-field ADVI -- the optimiser behind ``phylostan run -a vb`` (the
-default; ``phylostan/phylostan.py:302-317``: ``sm.vb(tol_rel_obj,
-elbo_samples, grad_samples, iter, eta, algorithm='meanfield')``).
+"""ADVI -- the optimiser behind ``phylostan run -a vb`` (the default;
+``phylostan/phylostan.py:302-317``: ``sm.vb(tol_rel_obj, elbo_samples,
+grad_samples, iter, eta, algorithm=arg.variational)`` with
+``-q meanfield|fullrank``).
 
-Algorithm: Stan's ``advi<Model, normal_meanfield>``: the approximation
-N(mu, diag(exp(omega)^2)) starts at the initial point with omega = 0;
+Algorithm: Stan's ``advi<Model, normal_meanfield>`` and ``advi<Model,
+normal_fullrank>``.  Mean-field: N(mu, diag(exp(omega)^2)) starting at the
+initial point with omega = 0.  Full-rank: N(mu, L L^T) with L lower
+triangular, starting at L = I; zeta = mu + L eta, entropy
+dim/2 (1 + log 2 pi) + sum log|L_dd|, gradient wrt L the lower triangle of
+mean(g eta^T) plus 1/L_dd on the diagonal.  Both:
 ``adapt_eta`` tries eta in (100, 10, 1, 0.1, 0.01) for ``adapt_iter`` (50)
 steps each; ``stochastic_gradient_ascent`` uses the adaGrad-like sequence
 (history 0.9 / 0.1, tau 1, eta / sqrt(iter)); every ``eval_elbo`` (100)
@@ -12,7 +17,12 @@ relative ELBO change goes into a circular buffer of
 max(0.1 max_iter / eval_elbo, 2) entries whose mean or median below
 ``tol_rel_obj`` stops the run.  The ELBO uses ``log_prob<propto=false>``
 (constants included), the gradient ``log_prob<propto=true>``; the entropy
-is ``dim/2 (1 + log 2 pi) + sum omega``.
+is ``dim/2 (1 + log 2 pi) + sum omega``.  Failed evaluations follow Stan:
+``calc_ELBO`` drops a non-finite draw without replacing it and still divides
+by ``elbo_samples`` (it gives up once ``elbo_samples`` draws were dropped);
+``calc_grad`` throws on the first non-finite gradient draw, which eta
+adaptation catches (zero gradient for that iteration) and stochastic
+gradient ascent does not.
 
 MI355X shape: the ``elbo_samples`` draws of each ELBO estimate (default 100)
 are ONE batched likelihood launch, as are the ``grad_samples`` draws of each
@@ -31,6 +41,8 @@ class ADVIError(RuntimeError):
 
 
 class MeanField:
+    family = "meanfield"
+
     def __init__(self, mu, omega=None):
         self.mu = np.asarray(mu, np.float64).copy()
         self.omega = np.zeros_like(self.mu) if omega is None else np.asarray(omega, np.float64).copy()
@@ -47,6 +59,52 @@ class MeanField:
     def sample(self, rng, n):
         return self.transform(rng.standard_normal((n, len(self.mu))))
 
+    def grad(self, G, eta):
+        """(d mu, d omega) of the ELBO from gradient draws G at transform(eta)."""
+        n = G.shape[0]
+        mu_g = G.sum(axis=0) / n
+        om_g = (G * eta).sum(axis=0) / n
+        return mu_g, om_g * np.exp(self.omega) + 1.0
+
+    def params(self):
+        return [self.mu, self.omega]
+
+
+class FullRank:
+    """normal_fullrank: N(mu, L L^T), L lower triangular (Cholesky factor)."""
+    family = "fullrank"
+
+    def __init__(self, mu, L=None):
+        self.mu = np.asarray(mu, np.float64).copy()
+        d = len(self.mu)
+        self.L = np.eye(d) if L is None else np.tril(np.asarray(L, np.float64)).copy()
+
+    def copy(self):
+        return FullRank(self.mu, self.L)
+
+    def entropy(self):
+        return (0.5 * len(self.mu) * (1.0 + math.log(2.0 * math.pi))
+                + float(np.log(np.abs(np.diag(self.L))).sum()))
+
+    def transform(self, eta):
+        return self.mu + eta @ self.L.T
+
+    def sample(self, rng, n):
+        return self.transform(rng.standard_normal((n, len(self.mu))))
+
+    def grad(self, G, eta):
+        n = G.shape[0]
+        mu_g = G.sum(axis=0) / n
+        L_g = np.tril(G.T @ eta) / n
+        L_g[np.diag_indices_from(L_g)] += 1.0 / np.diag(self.L)
+        return mu_g, L_g
+
+    def params(self):
+        return [self.mu, self.L]
+
+
+FAMILIES = {"meanfield": MeanField, "fullrank": FullRank}
+
 
 class ADVI:
     def __init__(self, posterior, rng, grad_samples=1, elbo_samples=100, eval_elbo=100, log=print):
@@ -61,63 +119,45 @@ class ADVI:
 
     # ------------------------------------------------------------ estimates
     def calc_elbo(self, q):
-        """Monte-Carlo ELBO; non-finite draws are dropped and redrawn (at most
-        elbo_samples of them), as calc_ELBO does."""
-        need = self.elbo_samples
-        got, total, dropped = 0, 0.0, 0
-        while got < self.elbo_samples:
-            Z = q.sample(self.rng, need)
-            lp = self.post.log_prob(Z, propto=False)
-            self.n_lp += len(Z)
-            ok = np.isfinite(lp)
-            total += float(lp[ok].sum())
-            got += int(ok.sum())
-            dropped += int((~ok).sum())
-            if dropped >= self.elbo_samples:
-                raise ADVIError("The number of dropped evaluations has reached its maximum amount (%d)."
-                                % self.elbo_samples)
-            need = self.elbo_samples - got
-        return total / self.elbo_samples + q.entropy()
+        """Monte-Carlo ELBO (Stan ``calc_ELBO``): a draw whose log density is
+        not finite is dropped, not replaced; the sum is still divided by
+        ``elbo_samples``; ``elbo_samples`` drops end the estimate."""
+        Z = q.sample(self.rng, self.elbo_samples)
+        lp = self.post.log_prob(Z, propto=False)
+        self.n_lp += len(Z)
+        ok = np.isfinite(lp)
+        if int((~ok).sum()) >= self.elbo_samples:
+            raise ADVIError("The number of dropped evaluations has reached its maximum amount (%d)."
+                            % self.elbo_samples)
+        return float(lp[ok].sum()) / self.elbo_samples + q.entropy()
 
     def calc_elbo_grad(self, q):
+        """Stan ``normal_*::calc_grad``: ``grad_samples`` draws, one batched
+        launch; any non-finite gradient draw throws."""
         dim = len(q.mu)
-        mu_g = np.zeros(dim)
-        om_g = np.zeros(dim)
-        got, drops = 0, 0
-        while got < self.grad_samples:
-            need = self.grad_samples - got
-            eta = self.rng.standard_normal((need, dim))
-            Z = q.transform(eta)
-            lp, G = self.post.log_prob_grad(Z)
-            self.n_grad += need
-            for k in range(need):
-                if np.isfinite(lp[k]) and np.all(np.isfinite(G[k])):
-                    mu_g += G[k]
-                    om_g += G[k] * eta[k]
-                    got += 1
-                else:
-                    drops += 1
-                    if drops >= 10 * self.grad_samples:
-                        raise ADVIError("stan::variational::normal_meanfield::calc_grad: The number of dropped "
-                                        "evaluations has reached its maximum amount (%d)." % (10 * self.grad_samples))
-        mu_g /= self.grad_samples
-        om_g /= self.grad_samples
-        om_g = om_g * np.exp(q.omega) + 1.0
-        return mu_g, om_g
+        eta = self.rng.standard_normal((self.grad_samples, dim))
+        Z = q.transform(eta)
+        lp, G = self.post.log_prob_grad(Z)
+        self.n_grad += self.grad_samples
+        bad = ~(np.isfinite(lp) & np.all(np.isfinite(G), axis=1))
+        if bad.any():
+            raise ADVIError("stan::variational::normal_%s::calc_grad: The number of dropped evaluations has "
+                            "reached its maximum amount (%d). Your model may be either severely ill-conditioned "
+                            "or misspecified." % (q.family, self.grad_samples))
+        return q.grad(G, eta)
 
     @staticmethod
-    def _step(q, gm, go, hist_m, hist_o, it, eta, first):
-        if first:
-            hist_m += gm * gm
-            hist_o += go * go
-        else:
-            hist_m *= 0.9
-            hist_m += 0.1 * gm * gm
-            hist_o *= 0.9
-            hist_o += 0.1 * go * go
+    def _step(q, grads, hists, it, eta, first):
+        """adaGrad-like update of every variational parameter array,
+        elementwise (stochastic_gradient_ascent: history 0.9 / 0.1, tau 1)."""
         es = eta / math.sqrt(it)
-        q.mu += es * gm / (1.0 + np.sqrt(hist_m))
-        q.omega += es * go / (1.0 + np.sqrt(hist_o))
+        for x, g, h in zip(q.params(), grads, hists):
+            if first:
+                h += g * g
+            else:
+                h *= 0.9
+                h += 0.1 * g * g
+            x += es * g / (1.0 + np.sqrt(h))
 
     # ------------------------------------------------------------ phases
     def adapt_eta(self, q0, adapt_iter=50):
@@ -127,16 +167,15 @@ class ADVI:
             raise ADVIError("Cannot compute ELBO using the initial variational distribution.")
         self.log("Begin eta adaptation.")
         elbo_best, eta_best = -math.inf, 0.0
-        dim = len(q0.mu)
         for k, eta in enumerate(ETA_SEQUENCE):
             q = q0.copy()
-            hm, ho = np.zeros(dim), np.zeros(dim)
+            hists = [np.zeros_like(x) for x in q.params()]
             for it in range(1, adapt_iter + 1):
                 try:
-                    gm, go = self.calc_elbo_grad(q)
+                    grads = self.calc_elbo_grad(q)
                 except ADVIError:
-                    gm, go = np.zeros(dim), np.zeros(dim)
-                self._step(q, gm, go, hm, ho, it, eta, it == 1)
+                    grads = [np.zeros_like(x) for x in q.params()]
+                self._step(q, grads, hists, it, eta, it == 1)
                 m = k * adapt_iter + it
                 if m == 1 or m % adapt_iter == 0:
                     self.log("Iteration: %3d / %d [%3d%%]  (Adaptation)"
@@ -166,8 +205,7 @@ class ADVI:
     def sga(self, q, eta, tol_rel_obj, max_iterations, diag=None):
         """stochastic_gradient_ascent; ``diag(iter, seconds, elbo)`` per ELBO
         evaluation (the rows of the .diag file)."""
-        dim = len(q.mu)
-        hm, ho = np.zeros(dim), np.zeros(dim)
+        hists = [np.zeros_like(x) for x in q.params()]
         cb_size = int(max(0.1 * max_iterations / self.eval_elbo, 2.0))
         cb = []
         elbo, elbo_best = 0.0, -math.inf
@@ -177,8 +215,8 @@ class ADVI:
         it = 0
         while True:
             it += 1
-            gm, go = self.calc_elbo_grad(q)
-            self._step(q, gm, go, hm, ho, it, eta, it == 1)
+            grads = self.calc_elbo_grad(q)
+            self._step(q, grads, hists, it, eta, it == 1)
             done = False
             if it % self.eval_elbo == 0:
                 elbo_prev = elbo
@@ -213,8 +251,8 @@ class ADVI:
                 return q, it
 
     def run(self, q0_mu, eta=None, adapt_engaged=True, adapt_iter=50, tol_rel_obj=0.01,
-            max_iterations=10000, diag=None):
-        q0 = MeanField(q0_mu)
+            max_iterations=10000, diag=None, family="meanfield"):
+        q0 = FAMILIES[family](q0_mu)
         if adapt_engaged or eta is None:
             eta = self.adapt_eta(q0, adapt_iter)
         q, iters = self.sga(q0.copy(), eta, tol_rel_obj, max_iterations, diag)

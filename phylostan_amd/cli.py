@@ -6,13 +6,21 @@ by the GPU likelihood engine instead of pystan:
 
 * ``build -s SCRIPT ...`` writes SCRIPT as a JSON model description (the
   options that shape the model and the Stan parameter names it implies) in
-  place of the emitted Stan program; there is nothing to compile
-  (``--compile`` only checks that the HIP library loads), so no ``.pkl`` is
-  written.
+  place of the emitted Stan program.  ``--compile`` "compiles" it: the HIP
+  engine is loaded and the compiled-model artifact is written under the
+  reference's name, SCRIPT with ``.stan`` replaced by ``.pkl`` (or SCRIPT +
+  ``.pkl``; phylostan.py:154-161).  The artifact is JSON, never a pickle:
+  the model options, the engine library and its kernel-source hash.
+* ``run`` follows phylostan.py:292-300: if the artifact is missing or
+  ``--compile`` is given it is (re)built, otherwise the existing one is
+  loaded and its model is used -- a run whose flags describe a different
+  model than the artifact is refused (the reference would hand Stan a data
+  dict that does not fit the compiled model).
 * ``run -s SCRIPT -t TREE -i ALN -o OUT ...`` reads and indexes the data
   exactly as the reference (``phylostan_amd.data.load``), builds the host
-  posterior around ``TreeLikelihood`` and runs ``-a vb`` (mean-field ADVI)
-  or ``-a nuts``; it writes OUT (Stan-format sample CSV; ``OUT_{chain}.csv``
+  posterior around ``TreeLikelihood`` and runs ``-a vb`` (ADVI,
+  (``-q meanfield``, the default, or ``-q fullrank``), ``-a nuts`` or
+  ``-a hmc`` (static HMC); it writes OUT (Stan-format sample CSV; ``OUT_{chain}.csv``
   for several chains, as pystan), ``OUT.diag`` (vb), ``OUT.trees`` and prints
   the ``parse_log`` summary.
 * ``parse --samples CSV -t TREE -o OUT.trees`` post-processes a sample file.
@@ -104,6 +112,42 @@ def _spec(arg):
     return ModelSpec.from_args(arg)
 
 
+def artifact_path(script):
+    """phylostan.py:155-158 / :292-294: the compiled model's file name."""
+    binary = script.replace(".stan", ".pkl")
+    return script + ".pkl" if binary == script else binary
+
+
+def compile_artifact(spec, script):
+    """Load the HIP engine and write the compiled-model artifact (JSON)."""
+    import hashlib
+    from . import _lib
+    _lib.load()
+    src = os.path.join(os.path.dirname(os.path.abspath(__file__)), "csrc", "phylo_hip.hip")
+    h = hashlib.sha1()
+    if os.path.exists(src):
+        with open(src, "rb") as fp:
+            h.update(fp.read())
+    doc = {"phylostan_amd_compiled": 1, "script": script, "options": dict(vars(spec)),
+           "engine": _lib.LIB_PATH, "kernel_source_sha1": h.hexdigest()[:12],
+           "note": "compiled-model artifact of the GPU engine (JSON; replaces the pickled pystan StanModel)"}
+    path = artifact_path(script)
+    with open(path, "w") as fp:
+        json.dump(doc, fp, indent=1)
+    return path
+
+
+def load_artifact(script):
+    path = artifact_path(script)
+    with open(path) as fp:
+        doc = json.load(fp)
+    if not isinstance(doc, dict) or doc.get("phylostan_amd_compiled") != 1:
+        raise SystemExit("%s is not a compiled-model artifact of this engine" % path)
+    from . import _lib
+    _lib.load()
+    return doc
+
+
 def build(arg):
     spec = _spec(arg)
     doc = {"phylostan_amd_model": 1, "options": dict(vars(spec)),
@@ -111,9 +155,8 @@ def build(arg):
     with open(arg.script, "w") as fp:
         json.dump(doc, fp, indent=1)
     if arg.compile:
-        from . import _lib
-        _lib.load()
-        print("GPU engine: %s" % _lib.LIB_PATH)
+        path = compile_artifact(spec, arg.script)
+        print("GPU engine: %s (compiled model %s)" % (os.environ.get("PHYLO_HIP_LIB", "libphylo_hip.so"), path))
 
 
 def _read_script(path):
@@ -135,22 +178,23 @@ def load_run_data(arg):
 def run(arg, likelihood_factory=None, log=print):
     spec = _spec(arg)
     opts = _read_script(arg.script)
+    if likelihood_factory is None:  # the GPU engine: compiled-model artifact (phylostan.py:292-300)
+        if arg.compile or not os.path.lexists(artifact_path(arg.script)):
+            compile_artifact(spec, arg.script)
+        else:
+            opts = load_artifact(arg.script)["options"]
     if opts is not None:
         for k in ("model", "categories", "invariant", "clock", "estimate_rate", "coalescent", "heterochronous"):
             if opts.get(k) != getattr(spec, k):
-                raise SystemExit("run option %s=%r differs from the built script (%r)" % (k, getattr(spec, k),
-                                                                                         opts.get(k)))
+                raise SystemExit("run option %s=%r differs from the built model (%r)" % (k, getattr(spec, k),
+                                                                                        opts.get(k)))
     if not arg.input:
         raise SystemExit("an alignment (-i) is required")
-    if arg.algorithm == "hmc":
-        raise SystemExit("static HMC is not supported; use -a nuts")
-    if arg.variational != "meanfield" and arg.algorithm == "vb":
-        raise SystemExit("only the meanfield variational family is supported")
     d = load_run_data(arg)
     log("Number of sequences: {} length {} ".format(d.S, int(np.sum(d.weights))))
     log("Model: " + arg.model)
     C = spec.C
-    chains = max(1, arg.chains) if arg.algorithm == "nuts" else 1
+    chains = max(1, arg.chains) if arg.algorithm in ("nuts", "hmc") else 1
     max_draws = max(arg.elbo_samples, arg.grad_samples, chains, 1)
     if likelihood_factory is None:
         from .engine import TreeLikelihood
@@ -158,7 +202,13 @@ def run(arg, likelihood_factory=None, log=print):
         lik = TreeLikelihood(d.tipcodes, d.weights, d.peel0, d.rooted, arg.model, C, max_draws=max_draws, device=dev)
     else:
         lik = likelihood_factory(d.tipcodes, d.weights, d.peel0, d.rooted, arg.model, C)
-    post = Posterior(spec, TreeData.from_phylodata(d), lik)
+    tree = TreeData.from_phylodata(d)
+    if not spec.heterochronous:
+        # --dates alone dates the tips (setup_dates) but, as in the reference,
+        # only --heterochronous puts lowers / lower_root into the model's data
+        # (phylostan.py:259-263): the model stays homochronous
+        tree = TreeData(d.S, d.peel0, d.map, None, None)
+    post = Posterior(spec, tree, lik)
     seed = arg.seed if arg.seed is not None else int(time.time()) % 100000
     rng = np.random.default_rng(seed)
     names = post.column_names()
@@ -171,16 +221,17 @@ def run(arg, likelihood_factory=None, log=print):
         from .advi import ADVI
         diag = stan_io.DiagWriter(sample_path + ".diag", config)
         adv = ADVI(post, rng, grad_samples=arg.grad_samples, elbo_samples=arg.elbo_samples, log=log)
-        q0 = post.initial_point(rng)
+        q0 = post.initialize(rng)
         t0 = time.time()
         q, eta, iters = adv.run(q0, eta=arg.eta, adapt_engaged=arg.eta is None, tol_rel_obj=arg.tol_rel_obj,
-                                max_iterations=arg.iter, diag=diag)
+                                max_iterations=arg.iter, diag=diag, family=arg.variational)
         diag.close()
         log("TIME: %.3f" % (time.time() - t0))
         mean_row = post.flat_rows(q.mu[None])[0]
         draws = post.flat_rows(q.sample(rng, arg.samples)) if arg.samples > 0 else np.zeros((0, len(names)))
         stan_io.write_vb_csv(sample_path, names, mean_row, draws,
-                             config + [("iter", iters), ("eta", eta), ("elbo_samples", arg.elbo_samples),
+                             config + [("algorithm", arg.variational), ("iter", iters), ("eta", eta),
+                                       ("elbo_samples", arg.elbo_samples),
                                        ("grad_samples", arg.grad_samples), ("tol_rel_obj", arg.tol_rel_obj),
                                        ("output_samples", arg.samples)], eta)
         stan_io.convert_samples_to_nexus(d.tree, sample_path, tree_path, arg.rate)
@@ -189,10 +240,10 @@ def run(arg, likelihood_factory=None, log=print):
     from .nuts import run_chains
     num_warmup = arg.iter // 2
     num_samples = arg.iter - num_warmup
-    q0s = [post.initial_point(np.random.default_rng((seed, c, 0))) for c in range(chains)]
+    q0s = [post.initialize(np.random.default_rng((seed, c, 0))) for c in range(chains)]
     t0 = time.time()
     res = run_chains(post, q0s, [(seed, c) for c in range(chains)], num_warmup=num_warmup,
-                     num_samples=num_samples, thin=arg.thin, progress=log)
+                     num_samples=num_samples, thin=arg.thin, progress=log, algorithm=arg.algorithm)
     el = time.time() - t0
     for c, ch in enumerate(res):
         rows = post.flat_rows(np.stack([dr[0] for dr in ch.draws]))
@@ -203,7 +254,7 @@ def run(arg, likelihood_factory=None, log=print):
         stan_io.write_nuts_csv(path, names, ch, rows,
                                config + [("chain", c), ("num_warmup", num_warmup), ("num_samples", num_samples),
                                          ("thin", arg.thin), ("gradient_evaluations", ch.n_grad)],
-                               elapsed=(el / 2, el / 2))
+                               elapsed=(el / 2, el / 2), algorithm=arg.algorithm)
         stan_io.convert_samples_to_nexus(d.tree, path, tpath, arg.rate)
         stan_io.parse_log(path, 0.05)
     return post

@@ -16,11 +16,27 @@ substitute a shard evaluator (gloo, world size 2) for the HIP one.
 import numpy as np
 
 
-def shard_range(P, rank, world):
-    """Contiguous pattern range [p0, p1) of ``rank`` (sizes differ by <= 1)."""
-    base, extra = divmod(P, world)
-    p0 = rank * base + min(rank, extra)
-    return p0, p0 + base + (1 if rank < extra else 0)
+ALIGN = 128  # patterns per sweep block at two columns per lane
+
+
+def shard_range(P, rank, world, align=ALIGN):
+    """Contiguous pattern range [p0, p1) of ``rank``.
+
+    Whole ``align``-pattern blocks are dealt out as evenly as possible (block
+    counts differ by <= 1) so every shard but the last starts and ends on a
+    sweep-block boundary and no rank carries a ragged block in the middle of
+    the alignment; the last rank takes the ragged tail.  With fewer blocks
+    than ranks the count-balanced split is used instead.
+    """
+    nblk = -(-P // align)
+    if nblk < world:
+        base, extra = divmod(P, world)
+        p0 = rank * base + min(rank, extra)
+        return p0, p0 + base + (1 if rank < extra else 0)
+    base, extra = divmod(nblk, world)
+    b0 = rank * base + min(rank, extra)
+    b1 = b0 + base + (1 if rank < extra else 0)
+    return min(P, b0 * align), min(P, b1 * align)
 
 
 class ShardedLikelihood:
@@ -49,10 +65,19 @@ class ShardedLikelihood:
     def outlen(self):
         return self.engine.outlen
 
-    def evaluate(self, blens, model, out, site_ll=None, stream=0, group=None):
-        """blens [n, B], model [n, 10+2C], out [n, outlen]: device tensors."""
+    def evaluate(self, blens, model, out, site_ll=None, stream=None, group=None):
+        """blens [n, B], model [n, 10+2C], out [n, outlen]: device tensors.
+
+        The sweep runs on ``stream`` (default: torch's current stream of
+        ``out``'s device), the stream RCCL's ``all_reduce`` orders itself
+        against, so the reduction reads ``out`` only after the kernels wrote
+        it and the kernels read blens / model only after torch produced them.
+        """
+        import torch
         import torch.distributed as dist
         n = blens.shape[0]
+        if stream is None:
+            stream = torch.cuda.current_stream(out.device).cuda_stream if out.is_cuda else 0
         self.engine.evaluate_device(blens.data_ptr(), model.data_ptr(), out.data_ptr(),
                                     site_ll.data_ptr() if site_ll is not None else 0, n_draws=n,
                                     stream=stream)

@@ -300,12 +300,82 @@ class Chain:
         return self
 
 
+class StaticHMCChain(Chain):
+    """Stan's ``adapt_diag_e_static_hmc`` (``sm.sampling(algorithm='HMC')``,
+    phylostan.py:319-321): a fixed integration time T (``int_time``, Stan's
+    default 2 pi) covered by L = max(1, int(T / eps)) leapfrog steps, one
+    Metropolis accept/reject of the end point (accept_stat = min(1,
+    exp(H0 - h)), NaN energy = rejection), and the same step-size and
+    diagonal-metric adaptation as NUTS (after every adaptation update L is
+    recomputed from the nominal step size; ``init_stepsize`` leaves it
+    alone, as ``base_hmc::init_stepsize`` does).  The draw record keeps the
+    NUTS layout with int_time in the tree-depth slot and divergent = 0."""
+
+    def __init__(self, dim, q0, rng, num_warmup=1000, num_samples=1000, thin=1, int_time=2 * math.pi, **kw):
+        kw.pop("max_depth", None)
+        super().__init__(dim, q0, rng, num_warmup, num_samples, thin, **kw)
+        self.T = float(int_time)
+        self._update_L()
+
+    def _update_L(self):
+        self.L = max(1, int(self.T / self.eps))
+
+    def _transition(self, z0):
+        z = z0.copy()
+        z.p = self._sample_p()
+        z_init = z.copy()
+        H0 = self._H(z)
+        n_lf = self.L
+        for _ in range(n_lf):
+            yield from self._evolve(z, self.eps)
+        h = self._H(z)
+        if math.isnan(h):
+            h = math.inf
+        accept = math.exp(H0 - h) if h != math.inf else 0.0
+        if accept < 1.0 and self.rng.uniform() > accept:
+            z = z_init
+        accept = min(1.0, accept)
+        return z, accept, self.T, n_lf, False, self._H(z)
+
+    def program(self):
+        lp, g = yield self.q0
+        z = _Point(self.q0.copy(), np.zeros(self.dim), lp, g)
+        if not np.isfinite(lp):
+            raise RuntimeError("HMC: initial point has non-finite log density")
+        yield from self._init_stepsize(z)
+        self._da_restart()
+        total = self.num_warmup + self.num_samples
+        for it in range(total):
+            warm = it < self.num_warmup
+            eps_used = self.eps
+            z_new, accept, int_time, n_lf, div, energy = yield from self._transition(z)
+            z = _Point(z_new.q, np.zeros(self.dim), z_new.lp, z_new.g)
+            if warm:
+                self._learn_stepsize(accept)
+                self._update_L()
+                if self._learn_variance(z.q):
+                    yield from self._init_stepsize(z)
+                    self._update_L()
+                    self._da_restart()
+                if it == self.num_warmup - 1:
+                    self.eps = math.exp(self.x_bar)  # complete_adaptation
+                    self._update_L()
+            if it % self.thin == 0:
+                self.draws.append((z.q.copy(), z.lp, accept, eps_used, int_time, n_lf, 0, energy, warm))
+        return self
+
+
 def run_chains(posterior, q0s, seeds, num_warmup=1000, num_samples=1000, thin=1, progress=None,
-               max_depth=10, **kw):
-    """Run ``len(q0s)`` NUTS chains in lockstep, batching every round of
-    gradient requests into one ``posterior.log_prob_grad`` call."""
-    chains = [Chain(posterior.dim, q0, np.random.default_rng(sd), num_warmup, num_samples, thin,
-                    max_depth=max_depth, **kw) for q0, sd in zip(q0s, seeds)]
+               max_depth=10, algorithm="nuts", **kw):
+    """Run ``len(q0s)`` NUTS (or static HMC) chains in lockstep, batching
+    every round of gradient requests into one ``posterior.log_prob_grad``
+    call."""
+    if algorithm == "hmc":
+        chains = [StaticHMCChain(posterior.dim, q0, np.random.default_rng(sd), num_warmup, num_samples, thin, **kw)
+                  for q0, sd in zip(q0s, seeds)]
+    else:
+        chains = [Chain(posterior.dim, q0, np.random.default_rng(sd), num_warmup, num_samples, thin,
+                        max_depth=max_depth, **kw) for q0, sd in zip(q0s, seeds)]
     gens = [c.program() for c in chains]
     pending = {}
     for i, g in enumerate(gens):
@@ -323,6 +393,6 @@ def run_chains(posterior, q0s, seeds, num_warmup=1000, num_samples=1000, thin=1,
                 del pending[i]
         rounds += 1
         if progress and rounds % 2000 == 0:
-            progress("NUTS: %d batched gradient rounds, %d draws (chain 0), %.1f s"
-                     % (rounds, len(chains[0].draws), time.time() - t0))
+            progress("%s: %d batched gradient rounds, %d draws (chain 0), %.1f s"
+                     % (algorithm.upper(), rounds, len(chains[0].draws), time.time() - t0))
     return chains

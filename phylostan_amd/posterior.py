@@ -33,6 +33,7 @@ import numpy as np
 from . import clocks
 from . import models
 from . import priors
+from . import transforms
 from .transforms import Identity, Lower, Simplex, Unit
 
 
@@ -414,10 +415,49 @@ class Posterior:
         return self._span(self._heights(vals, n)) * self._multiplier(vals, n)[0]
 
     # ------------------------------------------------------- value + gradient
+    def in_support(self, U):
+        """Rows of U whose constrained parameters are finite and strictly
+        inside their declared bounds (a draw outside is a Stan domain
+        error: rejected with lp = -inf before anything is evaluated)."""
+        U = np.atleast_2d(np.asarray(U, np.float64))
+        n = U.shape[0]
+        ok = np.all(np.isfinite(U), axis=1)
+        with np.errstate(all="ignore"):
+            vals, _, logj = self.constrain(np.where(np.isfinite(U), U, 0.0))
+            ok &= np.isfinite(logj)
+            for p in self.params:
+                x = np.asarray(vals[p.name], np.float64).reshape(n, -1)
+                ok &= np.all(np.isfinite(x), axis=1)
+                if isinstance(p.tr, transforms.Lower):
+                    ok &= np.all(x > p.tr.lower, axis=1)
+                elif isinstance(p.tr, transforms.Unit):
+                    ok &= np.all((x > 0.0) & (x < 1.0), axis=1)
+                elif isinstance(p.tr, transforms.Simplex):
+                    ok &= np.all(x > 0.0, axis=1)
+        return ok
+
     def log_prob_grad(self, U, propto=True, need_grad=True):
         """(lp [n], grad [n, dim]) at unconstrained draws U [n, dim]
-        (Jacobian included, as Stan's ``log_prob<propto, jacobian=true>``)."""
+        (Jacobian included, as Stan's ``log_prob<propto, jacobian=true>``).
+
+        Out-of-support draws (``in_support``) are rejected up front: lp =
+        -inf, zero gradient, and neither the transforms' numpy nor the GPU
+        sees them.  Draws in support whose arithmetic still overflows are
+        rejected the same way after evaluation."""
         U = np.atleast_2d(np.asarray(U, np.float64))
+        n = U.shape[0]
+        ok = self.in_support(U)
+        lp = np.full(n, -np.inf)
+        G = np.zeros((n, self.dim)) if need_grad else None
+        if ok.any():
+            with np.errstate(all="ignore"):
+                lp_ok, g_ok = self._log_prob_grad_rows(U[ok], propto, need_grad)
+            lp[ok] = lp_ok
+            if need_grad:
+                G[ok] = g_ok
+        return lp, G
+
+    def _log_prob_grad_rows(self, U, propto=True, need_grad=True):
         n = U.shape[0]
         sp = self.spec
         S, C = self.S, self.C
@@ -433,9 +473,7 @@ class Posterior:
             h = self._heights(vals, n)
             span = self._span(h)
             mult, subs = self._multiplier(vals, n)
-            # extreme draws may overflow here; they are rejected just below
-            with np.errstate(over="ignore", invalid="ignore"):
-                blens = span * mult
+            blens = span * mult  # an overflow here is rejected just below
         else:
             blens = vals["blens"]
 
@@ -618,6 +656,18 @@ class Posterior:
     def initial_point(self, rng, radius=2.0):
         """Stan's default initialisation: uniform(-2, 2) on the unconstrained scale."""
         return rng.uniform(-radius, radius, self.dim)
+
+    def initialize(self, rng, radius=2.0, max_tries=100):
+        """Stan ``services::util::initialize`` with random inits: up to 100
+        uniform(-2, 2) draws until the log density and its gradient are both
+        finite; the draw that passes is the initial point."""
+        for _ in range(max_tries):
+            q = self.initial_point(rng, radius)
+            lp, G = self.log_prob_grad(q[None])
+            if np.isfinite(lp[0]) and np.all(np.isfinite(G[0])):
+                return q
+        raise RuntimeError("Initialization failed after %d attempts: no random initial point with a finite log "
+                           "density and gradient" % max_tries)
 
     def props_from_heights(self, heights):
         """Inverse of the height transform: ``props`` reproducing ``heights``

@@ -17,19 +17,22 @@ import sys
 import numpy as np
 
 NUTS_COLUMNS = ["accept_stat__", "stepsize__", "treedepth__", "n_leapfrog__", "divergent__", "energy__"]
+HMC_COLUMNS = ["accept_stat__", "stepsize__", "int_time__", "energy__"]  # diag_e_static_hmc
 
 
 def _fmt(v):
     return "%.6g" % v
 
 
-def write_nuts_csv(path, colnames, chain, rows, config, elapsed=None, save_warmup=False):
+def write_nuts_csv(path, colnames, chain, rows, config, elapsed=None, save_warmup=False, algorithm="nuts"):
     """``rows``: [n_draws, len(colnames)] constrained values of the recorded
-    draws of ``chain`` (a ``nuts.Chain``), in the same order."""
+    draws of ``chain`` (a ``nuts.Chain`` or ``nuts.StaticHMCChain``), in the
+    same order.  Static HMC writes Stan's HMC sampler columns."""
+    hmc = algorithm == "hmc"
     with open(path, "w") as fp:
         for k, v in config:
             fp.write("# %s = %s\n" % (k, v))
-        fp.write(",".join(["lp__"] + NUTS_COLUMNS + colnames) + "\n")
+        fp.write(",".join(["lp__"] + (HMC_COLUMNS if hmc else NUTS_COLUMNS) + colnames) + "\n")
         adapt_written = False
         for d, vals in zip(chain.draws, rows):
             q, lp, acc, eps, depth, nlf, div, energy, warm = d
@@ -39,8 +42,11 @@ def write_nuts_csv(path, colnames, chain, rows, config, elapsed=None, save_warmu
                 fp.write("# Adaptation terminated\n# Step size = %g\n# Diagonal elements of inverse mass matrix:\n# %s\n"
                          % (chain.eps, ", ".join("%g" % x for x in chain.inv_metric)))
                 adapt_written = True
-            fp.write(",".join([_fmt(lp), _fmt(acc), _fmt(eps), "%d" % depth, "%d" % nlf, "%d" % div, _fmt(energy)]
-                              + [_fmt(x) for x in vals]) + "\n")
+            if hmc:  # the depth slot holds int_time
+                sampler = [_fmt(lp), _fmt(acc), _fmt(eps), _fmt(depth), _fmt(energy)]
+            else:
+                sampler = [_fmt(lp), _fmt(acc), _fmt(eps), "%d" % depth, "%d" % nlf, "%d" % div, _fmt(energy)]
+            fp.write(",".join(sampler + [_fmt(x) for x in vals]) + "\n")
         if elapsed is not None:
             w, s = elapsed
             fp.write("# \n#  Elapsed Time: %g seconds (Warm-up)\n#                %g seconds (Sampling)\n"
@@ -231,6 +237,37 @@ def parse_log(inputfile, alpha=0.05, tree=None, out=None):
         m, md, lo, hi = descriptive_stats(data[:, idx_root], alpha)
         res["root_height"] = (m, md, lo, hi)
         print("Root height mean: {} {}% CI: ({},{})".format(m, pct, lo, hi), file=out)
+        if tree is not None and "substrates.1" in header:
+            # relaxed clock (utils.py:354-380): per draw the mean rate
+            # sum(rate * time) / sum(time) over the branches; the "variance"
+            # is numpy.var of every branch rate seen in this and all earlier
+            # draws (the reference's list is never reset between draws)
+            rindex = header.index("substrates.1")
+            hindex = header.index("heights.1")
+            S = len(tree.taxon_namespace)
+            nodes = list(tree.postorder_node_iter())
+            mean_rates, variances, rates = [], [], []
+            for i in range(data.shape[0]):
+                for n in nodes:
+                    if not n.is_leaf():
+                        n.date = data[i, hindex + n.index - S - 1]
+                    if n.parent_node is not None:
+                        n.rate = data[i, rindex + n.index - 1]
+                        rates.append(n.rate)
+                dist = tm = 0.0
+                for n in nodes:
+                    if n.parent_node is not None:
+                        el = n.parent_node.date - n.date
+                        dist += n.rate * el
+                        tm += el
+                mean_rates.append(dist / tm)
+                variances.append(np.var(rates))
+            m, md, lo, hi = descriptive_stats(mean_rates, alpha)
+            res["mean_rate"] = (m, md, lo, hi)
+            print("Mean rate mean: {} {}% CI: ({},{})".format(m, pct, lo, hi), file=out)
+            m, md, lo, hi = descriptive_stats(variances, alpha)
+            res["variance_rate"] = (m, md, lo, hi)
+            print("Variance rate mean: {} {}% CI: ({},{})".format(m, pct, lo, hi), file=out)
     else:
         idx = [k for k, h in enumerate(header) if h.startswith("blens")]
         sums = data[:, idx].sum(axis=1)

@@ -69,16 +69,16 @@ def simulate(n_taxa=128, n_sites=1_000_000, C=4, wshape=0.5, gap_frac=0.01, seed
             continue
         blens[nd.index - 1] = nd.edge_length
         parent = states[nd.parent_node]
-        child = np.empty(n_sites, dtype=np.uint8)
         u = rng.random(n_sites)
+        # cumulative transition rows of every (category, parent state), then
+        # one gather per site: child = #{thresholds below u}
+        cum = np.empty((C, 4, 4))
         for c in range(C):
             P = (V * np.exp(lam * nd.edge_length * rs[c])[None, :]) @ Vinv
-            cum = np.cumsum(np.clip(P, 0.0, None), axis=1)
-            cum /= cum[:, -1:]
-            sel = cat == c
-            cp = cum[parent[sel]]
-            child[sel] = (u[sel, None] > cp[:, :3]).sum(1).astype(np.uint8)
-        states[nd] = child
+            cum[c] = np.cumsum(np.clip(P, 0.0, None), axis=1)
+            cum[c] /= cum[c][:, -1:]
+        cp = cum.reshape(C * 4, 4)[cat * 4 + parent]
+        states[nd] = (u[:, None] > cp[:, :3]).sum(1).astype(np.uint8)
     chars = np.empty((S, n_sites), dtype=np.uint8)
     lut = np.frombuffer(b"ACGT", dtype=np.uint8)
     for nd in tree.leaf_node_iter():

@@ -27,6 +27,22 @@ def load_kat():
         return json.load(fp)
 
 
+def load_phylo_points():
+    """HKY / GTR points evaluated by the reference's scripts/phylo.py
+    (tests/golden/make_golden.py, ``phylo_gtr_fixture``)."""
+    with open(os.path.join(GOLDEN, "phylo_gtr.json")) as fp:
+        return json.load(fp)["points"]
+
+
+def phylo_case(point):
+    """One scripts/phylo.py point as a C = 1 case on the dataset's compressed
+    layout (weights = column multiplicities, so sum w l = the reference's sum
+    over every alignment column)."""
+    d = load_layout(point["dataset"])
+    return Case("phylo_%s_%s" % (point["dataset"], point["model"]), d["tipbits"], d["weights"], d["peel"] - 1,
+                True, point["model"], 1, point["blens"], point["freqs"], point["rates"], [1.0], [1.0])
+
+
 class Case:
     """One likelihood problem in C-ABI conventions."""
 

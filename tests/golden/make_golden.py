@@ -13,6 +13,16 @@ What is taken from the reference (nothing here is restated by us):
   uses (``:323-329``), plus central finite-difference gradients of that same
   formula.  jax is absent, so ``jax`` / ``jax.numpy`` are bound to numpy for
   the duration of the import (the formula only calls ``exp`` and ``log``).
+* ``phylo_gtr.json`` -- HKY / GTR log-likelihoods computed by the
+  reference's own numpy pruner ``scripts/phylo.py`` (``GTR`` class
+  ``:4-61``: normalised Q, ``numpy.linalg.eig``; ``traverse`` /
+  ``compute_likelihood`` ``:240-296``: one rate category, every alignment
+  column, tips one-hot or all-ones) on the fluA and HCV trees with their
+  branch lengths times a clock rate.  The script is Python 2, so
+  ``builtins.xrange`` is bound to ``range`` for the import; the tree and
+  alignment objects are our DendroPy-compatible ones.  Per-site values are
+  read from the reference's root partials exactly as ``compute_likelihood``
+  forms them (``:285-290``).
 * ``<dataset>_layout.npz`` -- the Stan data layout that ``phylostan run``
   builds: ``phylostan/utils.py`` functions ``setup_indexes``,
   ``setup_dates``, ``get_peeling_order``, ``get_preorder``, ``get_lowers``
@@ -139,6 +149,71 @@ def layout_fixture(utils, tree_path, aln_path, heterochronous, rooted):
     return out
 
 
+def _import_reference_phylo():
+    import builtins
+    if not hasattr(builtins, "xrange"):
+        builtins.xrange = range
+    sys.path.insert(0, os.path.join(REF, "scripts"))
+    import phylo  # noqa: E402  (numpy + math only)
+    return phylo
+
+
+PHYLO_POINTS = [
+    # dataset, model, exchangeabilities (AC AG AT CG CT GT), freqs (None = empirical), clock rate
+    ("fluA", "HKY", [1.0, 5.58, 1.0, 1.0, 5.58, 1.0], None, 0.00499),
+    ("fluA", "GTR", [1.2, 4.1, 0.7, 0.9, 5.3, 1.0], [0.31, 0.19, 0.23, 0.27], 0.004),
+    ("HCV", "GTR", [0.125, 0.25, 0.125, 0.125, 0.25, 0.125], [0.25, 0.25, 0.25, 0.25], 7.9e-4),
+    ("HCV", "HKY", [1.0, 3.0, 1.0, 1.0, 3.0, 1.0], [0.22, 0.28, 0.26, 0.24], 1.2e-3),
+]
+
+
+def phylo_gtr_fixture(utils, phylo, specs):
+    """Log-likelihoods of the reference's scripts/phylo.py pruner."""
+    from phylostan_amd import data, models
+    out = {"source": "scripts/phylo.py:4-61 (GTR), :240-296 (traverse, compute_likelihood)",
+           "convention": "one category; branch length = input-tree edge length * clock_rate; node ids "
+                         "0-based as phylostan/utils.py setup_indexes minus one (tips in taxon-namespace "
+                         "order, internal nodes in post-order); site_ll per compressed pattern of the "
+                         "<dataset>_layout.npz fixture", "points": []}
+    for name, model, rates, freqs, clock in PHYLO_POINTS:
+        tpath, apath = specs[name][:2]
+        tree = treeio.read_tree(tpath)
+        tree.resolve_polytomies(update_bipartitions=True)
+        aln = treeio.read_alignment(apath)
+        rows = {t.label: _Seq(aln[t.label]) for t in tree.taxon_namespace}
+        alignment = _Alignment(rows)  # iteration = taxon-namespace order
+        for nd in tree.postorder_node_iter():
+            if nd.parent_node is not None:
+                nd.edge_length = nd.edge_length * clock
+        layout = np.load(os.path.join(HERE, "%s_layout.npz" % name), allow_pickle=False)
+        if freqs is None:
+            freqs = models.empirical_frequencies(layout["tipbits"], layout["weights"]).tolist()
+        gtr = phylo.GTR(list(rates), list(freqs))
+        total = phylo.compute_likelihood(tree, alignment, gtr)
+        # per-site values from the reference's own partials (compute_likelihood :283-290)
+        S = len(alignment)
+        partials = phylo.initialize_dna_partials(alignment)
+        matrices = np.zeros((2 * S - 2, 4, 4))
+        phylo.traverse(tree.seed_node, matrices, partials, gtr)
+        root = partials[2 * S - 2]
+        site = np.array([np.log(sum(root[i][j] * gtr.get_pi(j) for j in range(4)))
+                         for i in range(alignment.sequence_size)])
+        # map every site to its compressed pattern (first-seen order, raw symbols)
+        chars = np.array([[ord(ch) for ch in str(rows[t.label]).upper()] for t in tree.taxon_namespace],
+                         dtype=np.uint8)
+        _, _, first = data.compress_patterns(chars)
+        pat_ll = site[first]
+        blens = np.zeros(2 * S - 2)
+        for nd in tree.postorder_node_iter():
+            if nd.parent_node is not None:
+                blens[nd.index] = nd.edge_length
+        out["points"].append({"dataset": name, "model": model, "rates": list(rates), "freqs": list(freqs),
+                              "clock_rate": clock, "loglik": float(total), "site_ll": pat_ll.tolist(),
+                              "blens": blens.tolist()})
+        print(name, model, "reference loglik %.10f" % total)
+    return out
+
+
 def main():
     with open(os.path.join(HERE, "kat_3tax.json"), "w") as fp:
         json.dump(kat_fixture(), fp, indent=1)
@@ -153,6 +228,8 @@ def main():
         fx = layout_fixture(utils, tpath, apath, het, rooted)
         np.savez_compressed(os.path.join(HERE, "%s_layout.npz" % name), **fx)
         print(name, "S=%d P=%d sites=%d" % (fx["tipbits"].shape[0], fx["tipbits"].shape[1], fx["sites"]))
+    with open(os.path.join(HERE, "phylo_gtr.json"), "w") as fp:
+        json.dump(phylo_gtr_fixture(utils, _import_reference_phylo(), specs), fp)
 
 
 if __name__ == "__main__":

@@ -97,4 +97,33 @@ def test_shard_ranges_cover_and_balance():
             assert rs[0][0] == 0 and rs[-1][1] == P
             assert all(a[1] == b[0] for a, b in zip(rs, rs[1:]))
             sizes = [b - a for a, b in rs]
-            assert max(sizes) - min(sizes) <= 1
+            assert min(sizes) >= 1
+            if -(-P // 128) >= world:  # whole 128-pattern sweep blocks per rank
+                assert all(a % 128 == 0 for a, _ in rs)
+                blocks = [-(-(b - a) // 128) for a, b in rs]
+                assert max(blocks) - min(blocks) <= 1
+            else:
+                assert max(sizes) - min(sizes) <= 1
+
+
+def test_bench_spawns_one_rank_per_gpu():
+    """``python bench.py --gpus 2`` with no launcher starts two ranks through
+    torch.distributed.run (the driver's N>1 command); --dry-run stops after
+    the ranks joined a gloo group, before anything touches a GPU."""
+    import json
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ)
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK"):
+        env.pop(k, None)
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2", "--dry-run"],
+                       capture_output=True, text=True, timeout=300, env=env)
+    assert r.returncode == 0, r.stderr[-2000:]
+    line = [ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1]
+    rec = json.loads(line)
+    assert rec == {"dry_run": True, "n_gpus": 2, "sum_of_ranks": 1}
+    env["WORLD_SIZE"] = "3"
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2", "--dry-run"],
+                       capture_output=True, text=True, timeout=120, env=env)
+    assert r.returncode != 0 and "WORLD_SIZE" in r.stderr

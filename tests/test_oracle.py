@@ -191,3 +191,20 @@ def test_q_param_gradients_batch_matches_per_draw():
         a, b = models.q_param_gradients(G[d], bl[d], rs[d], f[d], rt[d], fr[d])
         np.testing.assert_allclose(gr[d], a, rtol=1e-12, atol=1e-12 * np.max(np.abs(a)))
         np.testing.assert_allclose(gf[d], b, rtol=1e-12, atol=1e-12 * np.max(np.abs(b)))
+
+
+@pytest.mark.parametrize("k", range(4))
+def test_oracle_vs_reference_phylo_py(k):
+    """HKY / GTR pinned to the reference's own pruner (scripts/phylo.py):
+    total and per-pattern log-likelihoods of the oracle (numpy and C) equal
+    the values the reference computed on the fluA / HCV trees."""
+    from oracle import cpu
+    pt = cases.load_phylo_points()[k]
+    case = cases.phylo_case(pt)
+    ref = case.oracle()
+    np.testing.assert_allclose(ref["site_ll"], pt["site_ll"], rtol=1e-10, atol=1e-12)
+    assert abs(ref["loglik"] - pt["loglik"]) <= 1e-10 * abs(pt["loglik"])
+    out, sl = cpu.evaluate(case.tipcodes, case.weights, case.peel0, True, npr.MODEL_IDS[case.model],
+                           case.model_vec(), case.blens, 1, site_ll=True)
+    np.testing.assert_allclose(sl, pt["site_ll"], rtol=1e-10, atol=1e-12)
+    assert abs(out[0] - pt["loglik"]) <= 1e-10 * abs(pt["loglik"])
