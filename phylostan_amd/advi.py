@@ -22,7 +22,8 @@ is ``dim/2 (1 + log 2 pi) + sum omega``.  Failed evaluations follow Stan:
 by ``elbo_samples`` (it gives up once ``elbo_samples`` draws were dropped);
 ``calc_grad`` throws on the first non-finite gradient draw, which eta
 adaptation catches (zero gradient for that iteration) and stochastic
-gradient ascent does not.
+gradient ascent does not -- here (documented in ``calc_elbo_grad``) a failed
+gradient draw is redrawn instead, up to 10 * grad_samples times.
 
 MI355X shape: the ``elbo_samples`` draws of each ELBO estimate (default 100)
 are ONE batched likelihood launch, as are the ``grad_samples`` draws of each
@@ -133,18 +134,32 @@ class ADVI:
 
     def calc_elbo_grad(self, q):
         """Stan ``normal_*::calc_grad``: ``grad_samples`` draws, one batched
-        launch; any non-finite gradient draw throws."""
+        launch.  Deliberate difference: Stan throws on the first draw whose
+        gradient is not finite (ending the run during stochastic gradient
+        ascent); here such a draw is redrawn, and only ``10 * grad_samples``
+        failed draws within one estimate end the run.  Draws whose
+        transforms overflow in this fp64 numpy host path are rejected
+        (``Posterior.in_support``) where Stan's autodiff may still have
+        produced a finite value, and one of them should not end a 30k
+        iteration run."""
         dim = len(q.mu)
-        eta = self.rng.standard_normal((self.grad_samples, dim))
-        Z = q.transform(eta)
-        lp, G = self.post.log_prob_grad(Z)
-        self.n_grad += self.grad_samples
-        bad = ~(np.isfinite(lp) & np.all(np.isfinite(G), axis=1))
-        if bad.any():
-            raise ADVIError("stan::variational::normal_%s::calc_grad: The number of dropped evaluations has "
-                            "reached its maximum amount (%d). Your model may be either severely ill-conditioned "
-                            "or misspecified." % (q.family, self.grad_samples))
-        return q.grad(G, eta)
+        got_G, got_eta = [], []
+        need, drops = self.grad_samples, 0
+        while need > 0:
+            eta = self.rng.standard_normal((need, dim))
+            Z = q.transform(eta)
+            lp, G = self.post.log_prob_grad(Z)
+            self.n_grad += need
+            ok = np.isfinite(lp) & np.all(np.isfinite(G), axis=1)
+            got_G.append(G[ok])
+            got_eta.append(eta[ok])
+            drops += int((~ok).sum())
+            need -= int(ok.sum())
+            if drops >= 10 * self.grad_samples:
+                raise ADVIError("stan::variational::normal_%s::calc_grad: The number of dropped evaluations "
+                                "has reached its maximum amount (%d). Your model may be either severely "
+                                "ill-conditioned or misspecified." % (q.family, 10 * self.grad_samples))
+        return q.grad(np.concatenate(got_G), np.concatenate(got_eta))
 
     @staticmethod
     def _step(q, grads, hists, it, eta, first):
