@@ -53,6 +53,8 @@ def parse():
     ap.add_argument("--wg-budget", type=int, default=0)
     ap.add_argument("--cols", type=int, default=0, help="pattern columns per lane (0 = automatic)")
     ap.add_argument("--lds-budget", type=int, default=0)
+    ap.add_argument("--engine", choices=["auto", "pattern", "class"], default="auto",
+                    help="pattern sweep, class sweep (site repeats) or the context's automatic choice")
     ap.add_argument("--json-out", default=None)
     ap.add_argument("--dry-run", action="store_true",
                     help="launcher check only: ranks join a gloo group on the CPU, all-reduce their rank "
@@ -62,8 +64,9 @@ def parse():
 
 def kernel_source_hash():
     h = hashlib.sha1()
-    with open(os.path.join(ROOT, "phylostan_amd", "csrc", "phylo_hip.hip"), "rb") as fp:
-        h.update(fp.read())
+    for name in ("phylo_hip.hip", "class_engine.inc"):
+        with open(os.path.join(ROOT, "phylostan_amd", "csrc", name), "rb") as fp:
+            h.update(fp.read())
     return h.hexdigest()[:12]
 
 
@@ -136,6 +139,18 @@ def algorithmic_bytes(S, P, C, nslots, B, draws):
     branch-category)."""
     per_draw = 64 * nslots * C * P + S * P // 2 + 8 * P + 256 * B * C
     return per_draw * draws
+
+
+def class_algorithmic_bytes(C, classes, stage, draws):
+    """HBM bytes of one class-sweep evaluation (DESIGN.md "Class sweep"):
+    per category, every non-root subtree class's moved partial is written
+    once (forward) and its aggregated upper partial written (RED) and read
+    (REV) once -- 3 x 32 B per class; every contribution a parent class makes
+    to an internal child is gathered in the forward, gathered again and
+    stored in the reverse, and read by the segmented reduction -- 4 x 32 B
+    per staging element (``stage`` = sum over internal nodes of classes x
+    internal children, the root's included)."""
+    return 32 * C * (3 * classes + 4 * stage) * draws
 
 
 def survey_bytes(S, P, C, draws):
@@ -291,10 +306,15 @@ def main():
     sl = ShardedLikelihood(prob["tipcodes"], prob["weights"], prob["peel0"], prob["rooted"], prob["model"],
                            C, shard_rank, shard_world, device=local, max_draws=draws)
     eng = sl.engine
+    if args.engine != "auto":
+        eng.set_engine(args.engine)
     if args.wg_budget or args.cols or args.lds_budget:
         eng.set_tuning(args.wg_budget, args.cols, args.lds_budget)
     info = eng.program_info()
     info.update(eng.lds_plan())
+    info["engine"] = eng.engine()
+    if info["engine"] == "class":
+        info.update({"class_" + k: v for k, v in eng.class_info().items()})
     B = eng.B
     P_local = sl.p1 - sl.p0
 
@@ -389,7 +409,12 @@ def main():
         tb = time.perf_counter()
         single = dict(evals_per_s=n1 / (tb - ta), us_per_eval=1e6 * (tb - ta) / n1)
 
-    alg = algorithmic_bytes(S, P_local, C, info["nslots"] - info.get("recomputed", 0), B, draws)
+    if info["engine"] == "class":
+        alg = class_algorithmic_bytes(C, info["class_classes"], info["class_stage"], draws)
+        kernel_name = "class sweep: cls_fwd/cls_root/cls_red/cls_fix/cls_rev kernels, forward through reverse"
+    else:
+        alg = algorithmic_bytes(S, P_local, C, info["nslots"] - info.get("recomputed", 0), B, draws)
+        kernel_name = "sweep_kernel"
     achieved = alg / (kern_avg_ms * 1e-3) / 1e9
     traffic = None
     pmc = os.path.join(ROOT, "profiles", "pmc_traffic.json")
@@ -397,7 +422,7 @@ def main():
         try:
             with open(pmc) as fp:
                 rec = json.load(fp)
-            key = "%s:%d" % (args.workload, draws)
+            key = "%s:%d:%s" % (args.workload, draws, info["engine"])
             if rec.get("kernel_source") == kernel_source_hash() and key in rec.get("per_launch_bytes", {}):
                 traffic = rec["per_launch_bytes"][key]
         except (OSError, ValueError):
@@ -441,7 +466,7 @@ def main():
             "roofline": {
                 "bound": "hbm", "achieved": achieved, "peak": PEAK_HBM_GBPS, "unit": "GB/s",
                 "frac": achieved / PEAK_HBM_GBPS, "traffic": traffic,
-                "kernel": "sweep_kernel", "kernel_avg_ms": kern_avg_ms,
+                "kernel": kernel_name, "kernel_avg_ms": kern_avg_ms,
                 "algorithmic_bytes_per_launch": alg,
                 "survey_model_bytes_per_launch": survey_bytes(S, P_local, C, draws),
             },

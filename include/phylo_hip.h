@@ -164,6 +164,26 @@ int phy_deep_stack_in_lds(const phy_ctx* ctx);
 int phy_set_recompute(phy_ctx* ctx, int on);
 int phy_recomputed_partials(const phy_ctx* ctx);
 
+/* Engine: 1 = pattern sweep (one lane per pattern column), 2 = class sweep
+ * (site repeats: the forward pass once per distinct tip-state tuple of each
+ * subtree, the reverse on upper partials aggregated per tuple -- the exact,
+ * total form of the reference's column-reuse cache, pruner/tree.cpp:140-174),
+ * 0 = automatic (class sweep for alignments of >= 16384 patterns whose
+ * subtree classes are at most a quarter of the pattern sweep's node-pattern
+ * work).  Results agree to rounding either way.  PHY_ENGINE sets the default
+ * at phy_create.  phy_engine returns the engine the next launch uses (0
+ * pattern, 1 class). */
+int phy_set_engine(phy_ctx* ctx, int mode);
+int phy_engine(const phy_ctx* ctx);
+
+/* Class-plan facts (zeros when no plan is built): non-root subtree classes
+ * (the class sweep's forward work per category), levels (the root's level),
+ * root classes (distinct site patterns by tip state), staging elements (sum
+ * over internal nodes of classes x internal children: the reverse's
+ * contributions), reduction tiles and tile-crossing segments. */
+int phy_class_info(const phy_ctx* ctx, long long* classes, int* levels, int* root_classes, long long* stage,
+                   int* tiles, int* spans);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1239,11 +1239,14 @@ __global__ void __launch_bounds__(256) finalize_kernel(FinArgs a) {
   const size_t wg0 = (size_t)draw * a.gx;
   const int og = 1 + B + 2 * C + 4;
   if (threadIdx.x < 16) Q[threadIdx.x] = a.eig[(size_t)draw * EIG_LEN + EIG_Q + threadIdx.x];
-  if (threadIdx.x < WAVE) {
-    // scalar partials per slot: [c][8] = ll (c = 0 only), dps_c, dfreq[4]
-    const int lane = threadIdx.x;
+  {
+    // scalar partials per slot: [c][8] = ll (c = 0 only), dps_c, dfreq[4];
+    // quantity q is summed by wave q mod (waves), lanes striding over the
+    // slots, then a fixed-shape wave reduction (the same order whichever
+    // wave does it)
+    const int lane = threadIdx.x & (WAVE - 1);
     const int nq = 2 + C + 4;  // ll, dps_0..C-1, dfreq_0..3 (+1 spare)
-    for (int q = 0; q < nq - 1; ++q) {
+    for (int q = threadIdx.x / WAVE; q < nq - 1; q += blockDim.x / WAVE) {
       double acc = 0.0;
       for (int w = lane; w < a.gx; w += WAVE) {
         const double* ss = a.sslot + (wg0 + w) * C * 8;
@@ -1317,6 +1320,11 @@ __global__ void __launch_bounds__(256) finalize_kernel(FinArgs a) {
 // ---------------------------------------------------------------------------
 // host side
 // ---------------------------------------------------------------------------
+namespace {
+struct ClassEngine;  // class_engine.inc
+void free_class_engine(ClassEngine* e);
+}  // namespace
+
 struct phy_ctx {
   int S, P, Ppad, C, B, rooted, kind, max_draws, device;
   int nsteps, nslots, ndeep, nblk, nmat;
@@ -1332,6 +1340,14 @@ struct phy_ctx {
   bool recompute = true;       // rebuild cherries in the reverse instead of storing them
   bool fin_pref = true;        // finalize inside the sweep when one workgroup runs a draw (PHY_FIN=0: off)
   int nrec = 0;                // cherries recomputed under the current plan
+  // engine: 0 = pattern sweep (sweep_kernel), 1 = class sweep (site repeats,
+  // class_engine.inc); engine_pref 0 = automatic, 1 = pattern, 2 = class
+  int engine = 0, engine_pref = 0;
+  ClassEngine* ce = nullptr;
+  std::vector<uint8_t> h_tips;  // host copies of the static data (the class plan is built on demand)
+  std::vector<double> h_w;
+  std::vector<int32_t> h_peel;
+  std::vector<int> vec_of, gpos;
   hipStream_t stream;
   std::vector<int> prog;  // host copy of the program (chunk fields per plan)
   uint8_t* d_tips = nullptr;
@@ -1370,6 +1386,7 @@ void free_ctx(phy_ctx* c) {
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   for (hipEvent_t e : c->ev) (void)hipEventDestroy(e);
+  free_class_engine(c->ce);
   if (c->stream) (void)hipStreamDestroy(c->stream);
   (void)hipSetDevice(dev_old);
   delete c;
@@ -1561,6 +1578,8 @@ int dalloc(T** p, size_t n) {
   return PHY_OK;
 }
 
+#include "class_engine.inc"
+
 constexpr size_t LDS_CAP = 160 * 1024;
 constexpr int MIN_CAP = 24;  // an occupancy level is taken only if chunks stay this large
 
@@ -1684,6 +1703,105 @@ int plan_chunks(phy_ctx* c) {
   return PHY_OK;
 }
 
+// Engine choice.  Pattern sweep (sweep_kernel) or class sweep
+// (class_engine.inc).  Automatic: the class plan is built only for large
+// alignments (P >= 16384 patterns) and kept when its non-root classes are at
+// most a quarter of the (node, pattern) work of the pattern sweep -- e.g. the
+// synthetic 128 x 1M workload (1.16M classes vs 66.5M); the small configs
+// (fluA / HCV / DS1, batched over draws) stay on the pattern sweep.
+int ensure_class_plan(phy_ctx* c) {
+  if (c->ce) return PHY_OK;
+  return build_class_engine(c->S, c->P, c->C, c->rooted, c->h_tips.data(), c->h_w.data(), c->h_peel.data(),
+                            c->vec_of, c->R, c->nmat, c->gpos, &c->ce);
+}
+
+int select_engine(phy_ctx* c) {
+  c->engine = 0;
+  if (c->engine_pref == 1) return PHY_OK;
+  if (c->engine_pref == 0 && c->P < 16384) return PHY_OK;
+  int rc = ensure_class_plan(c);
+  if (rc) return rc;
+  const double pattern_work = (double)(c->S - 2) * c->P;
+  if (c->engine_pref == 2 || (double)c->ce->classes <= 0.25 * pattern_work) {
+    c->engine = 1;
+  } else {
+    free_class_engine(c->ce);
+    c->ce = nullptr;
+  }
+  return PHY_OK;
+}
+
+// HIP events around the timed part of one launch (phy_timing_start)
+int timing_begin(phy_ctx* ctx, hipStream_t st, hipEvent_t* e0, hipEvent_t* e1) {
+  if (ctx->ev_used + 2 > (int)ctx->ev.size()) {
+    // pool full: fold what is recorded so far
+    HIP_TRY(hipStreamSynchronize(st));
+    for (int k = 0; k + 1 < ctx->ev_used; k += 2) {
+      float ms = 0.f;
+      HIP_TRY(hipEventElapsedTime(&ms, ctx->ev[k], ctx->ev[k + 1]));
+      ctx->timed_ms += ms;
+      ctx->timed_n += 1;
+    }
+    ctx->ev_used = 0;
+  }
+  *e0 = ctx->ev[ctx->ev_used];
+  *e1 = ctx->ev[ctx->ev_used + 1];
+  ctx->ev_used += 2;
+  HIP_TRY(hipEventRecord(*e0, st));
+  return PHY_OK;
+}
+
+// The class sweep (class_engine.inc): forward levels, root, reverse levels,
+// then the ordered dL/dP sums and the shared finalize.  The timed region
+// (phy_timing_*) spans the forward through the last reverse level.
+int launch_class(phy_ctx* ctx, int n, const double* d_blens, const double* d_model, double* d_out,
+                 double* d_site, hipStream_t st) {
+  ClassEngine* e = ctx->ce;
+  const int C = ctx->C, B = ctx->B;
+  if ((long)n * C > 65535) return fail(PHY_ERANGE, "class sweep: n_draws * C must be <= 65535");
+  int rc = class_engine_reserve(e, n);
+  if (rc) return rc;
+  ClassArgs a = class_args(e, ctx->d_pmat, d_model, ctx->extra);
+  const int dcn = n * C;
+  hipEvent_t e0 = nullptr, e1 = nullptr;
+  if (ctx->timing && (rc = timing_begin(ctx, st, &e0, &e1))) return rc;
+  for (int l = 1; l < e->levels; ++l) {
+    const ClassLevel& L = e->lv[l];
+    if (!L.nchunk) continue;
+    a.first = L.chunk0;
+    a.count = L.nchunk;
+    hipLaunchKernelGGL(cls_fwd_kernel, dim3((L.nchunk + 3) / 4, dcn), dim3(256), 0, st, a);
+  }
+  hipLaunchKernelGGL(cls_root_ll_kernel, dim3((e->nroot + 255) / 256, n), dim3(256), 0, st, a);
+  hipLaunchKernelGGL(cls_root_rev_kernel, dim3(e->nrootch, dcn), dim3(64), 0, st, a);
+  for (int l = e->levels - 1; l >= 1; --l) {
+    const ClassLevel& L = e->lv[l];
+    if (L.ntile) {
+      a.first = L.tile0;
+      a.count = L.ntile;
+      hipLaunchKernelGGL(cls_red_kernel, dim3((L.ntile + 3) / 4, dcn), dim3(256), 0, st, a);
+    }
+    if (L.nchunk) {
+      a.first = L.chunk0;
+      a.count = L.nchunk;
+      hipLaunchKernelGGL(cls_rev_kernel, dim3((L.nchunk + 3) / 4, dcn), dim3(256), 0, st, a);
+    }
+  }
+  HIP_TRY(hipGetLastError());
+  if (ctx->timing) HIP_TRY(hipEventRecord(e1, st));
+  hipLaunchKernelGGL(cls_gsum_kernel, dim3(B, dcn), dim3(256), 0, st, (const double*)e->d_gpart,
+                     (const int*)e->d_gbase, (const int*)e->d_gcount, d_out, B, C, std::max(e->ngs, 1),
+                     phy_output_len(ctx));
+  if (d_site)
+    hipLaunchKernelGGL(cls_site_kernel, dim3((ctx->P + 255) / 256, n), dim3(256), 0, st,
+                       (const double*)e->d_sitecls, (const int*)e->d_pat_root, d_site, ctx->P, e->nroot);
+  FinArgs fa{ctx->d_gslot, e->d_sslot, ctx->d_pmat, ctx->d_eig, d_blens, d_model, ctx->d_gpos, ctx->d_inner, d_out,
+             C,            B,          ctx->nmat,   e->nrootch,  phy_output_len(ctx), 0, ctx->R};
+  hipLaunchKernelGGL(finalize_kernel, dim3(n), dim3(256), ((size_t)C * B + 16) * sizeof(double), st, fa);
+  HIP_TRY(hipGetLastError());
+  return PHY_OK;
+}
+
 int launch(phy_ctx* ctx, int n, const double* d_blens, const double* d_model, double* d_out,
            double* d_site, hipStream_t st) {
   const int C = ctx->C, B = ctx->B;
@@ -1696,6 +1814,7 @@ int launch(phy_ctx* ctx, int n, const double* d_blens, const double* d_model, do
                        (size_t)PMAT_WAVE_RECS * ctx->R * 4 * sizeof(double), st, pa);
     HIP_TRY(hipGetLastError());
   }
+  if (ctx->engine == 1) return launch_class(ctx, n, d_blens, d_model, d_out, d_site, st);
   // persistent workgroups: the explicit budget, else exactly what is resident
   const int budget = ctx->wg_budget > 0 ? ctx->wg_budget : ctx->wg_resident;
   const int gx = std::max(1, std::min(ctx->nblk, (budget + n - 1) / n));
@@ -1712,21 +1831,8 @@ int launch(phy_ctx* ctx, int n, const double* d_blens, const double* d_model, do
                B,            phy_output_len(ctx), g_direct, ctx->extra, fin, d_blens};
   hipEvent_t e0 = nullptr, e1 = nullptr;
   if (ctx->timing) {
-    if (ctx->ev_used + 2 > (int)ctx->ev.size()) {
-      // pool full: fold what is recorded so far
-      HIP_TRY(hipStreamSynchronize(st));
-      for (int k = 0; k + 1 < ctx->ev_used; k += 2) {
-        float ms = 0.f;
-        HIP_TRY(hipEventElapsedTime(&ms, ctx->ev[k], ctx->ev[k + 1]));
-        ctx->timed_ms += ms;
-        ctx->timed_n += 1;
-      }
-      ctx->ev_used = 0;
-    }
-    e0 = ctx->ev[ctx->ev_used];
-    e1 = ctx->ev[ctx->ev_used + 1];
-    ctx->ev_used += 2;
-    HIP_TRY(hipEventRecord(e0, st));
+    int rc = timing_begin(ctx, st, &e0, &e1);
+    if (rc) return rc;
   }
   const int threads = C * WAVE;
   if (ctx->K == 2)
@@ -1913,6 +2019,7 @@ int phy_create(int S, int P, int C, int rooted, int model, const uint8_t* tipcod
       return fail(PHY_EINVAL, "internal: one matrix per branch expected");
     }
     for (int m = 0; m < c->nmat; ++m) gpos[mat_branch[m]] = m;
+    c->gpos = gpos;
     for (int b = 0; b < c->B; ++b)
       if (gpos[b] < 0) {
         std::string m_ = "internal: branch " + std::to_string(b) + " not in the program";
@@ -1929,6 +2036,15 @@ int phy_create(int S, int P, int C, int rooted, int model, const uint8_t* tipcod
     HIP_C(hipMemcpy(c->d_gpos, gpos.data(), gpos.size() * sizeof(int), hipMemcpyHostToDevice));
   }
   TRY_C(plan_chunks(c));
+  c->h_tips.assign(tipcodes, tipcodes + (size_t)S * P);
+  c->h_w.assign(weights, weights + P);
+  c->h_peel.assign(peel, peel + 3 * (S - 1));
+  c->vec_of = vec_of;
+  {
+    const char* ek = getenv("PHY_ENGINE");
+    c->engine_pref = ek ? std::max(0, std::min(2, atoi(ek))) : 0;
+  }
+  TRY_C(select_engine(c));
   *out = c;
   return PHY_OK;
 }
@@ -2065,6 +2181,35 @@ int phy_set_recompute(phy_ctx* ctx, int on) {
   return plan_chunks(ctx);
 }
 int phy_recomputed_partials(const phy_ctx* ctx) { return ctx ? ctx->nrec : -1; }
+
+int phy_set_engine(phy_ctx* ctx, int mode) {
+  if (!ctx) return fail(PHY_EINVAL, "NULL ctx");
+  if (mode < 0 || mode > 2) return fail(PHY_EINVAL, "engine must be 0 (automatic), 1 (pattern) or 2 (class)");
+  HIP_TRY(hipSetDevice(ctx->device));
+  HIP_TRY(hipStreamSynchronize(ctx->stream));
+  ctx->engine_pref = mode;
+  return select_engine(ctx);
+}
+
+int phy_engine(const phy_ctx* ctx) { return ctx ? ctx->engine : -1; }
+
+int phy_class_info(const phy_ctx* ctx, long long* classes, int* levels, int* root_classes, long long* stage,
+                   int* tiles, int* spans) {
+  if (!ctx) return fail(PHY_EINVAL, "NULL ctx");
+  const ClassEngine* e = ctx->ce;
+  long long ns = 0;
+  int nspan = 0;
+  if (e)
+    for (const ClassLevel& L : e->lv) nspan += L.nspan;
+  if (e) ns = e->stage_elems;
+  if (classes) *classes = e ? e->classes : 0;
+  if (levels) *levels = e ? e->levels : 0;
+  if (root_classes) *root_classes = e ? e->nroot : 0;
+  if (stage) *stage = ns;
+  if (tiles) *tiles = e ? e->ntiles : 0;
+  if (spans) *spans = nspan;
+  return PHY_OK;
+}
 
 int phy_lds_plan(const phy_ctx* ctx, int* n_chunks, int* matrices_per_chunk, int* lds_bytes_out) {
   if (!ctx) return fail(PHY_EINVAL, "NULL ctx");

@@ -1,0 +1,130 @@
+"""GPU parity of the class sweep (site repeats, SURVEY.md 8a row a10 --
+the exact form of the reference's column-reuse cache, pruner/tree.cpp:140-174)
+against the CPU oracle, through the C-ABI with phy_set_engine(2).
+
+Same bar as tests/test_gpu_parity.py: per-site and total log L rel 1e-10,
+every gradient rel 1e-9 of its array's largest entry.
+"""
+import numpy as np
+import pytest
+
+from tests import cases
+from tests.test_gpu_parity import RTOL_G, RTOL_LL, _close, _engine, check_case
+
+pytestmark = pytest.mark.gpu
+
+
+def _class_engine(case, max_draws=1):
+    eng = _engine(case, max_draws=max_draws)
+    eng.set_engine("class")
+    assert eng.engine() == "class"
+    return eng
+
+
+@pytest.mark.parametrize("make", [cases.fluA_case, cases.hcv_case, cases.ds1_case],
+                         ids=["fluA_HKY_W4", "HCV_GTR_W4", "DS1_JC69_unrooted"])
+def test_class_sweep_config_datasets(make):
+    case = make()
+    eng = _class_engine(case)
+    info = eng.class_info()
+    assert 0 < info["classes"] < (case.S - 2) * case.P
+    check_case(case, eng)
+
+
+@pytest.mark.parametrize("seed,S,P,C,model,rooted,cat", [
+    (1, 5, 1, 1, "JC69", True, False),       # single pattern
+    (2, 12, 63, 3, "GTR", True, False),
+    (3, 12, 130, 4, "HKY", True, False),
+    (4, 17, 257, 5, "GTR", False, False),    # unrooted
+    (5, 40, 200, 2, "GTR", True, True),      # caterpillar
+    (6, 40, 200, 4, "JC69", False, True),    # unrooted caterpillar
+    (7, 128, 3000, 4, "GTR", True, False),   # long segments, many tiles
+    (8, 9, 100, 8, "HKY", True, False),
+    (9, 300, 500, 4, "GTR", True, False),    # many levels
+])
+def test_class_sweep_random_trees(seed, S, P, C, model, rooted, cat):
+    case = cases.random_case(seed, S=S, P=P, C=C, model=model, rooted=rooted, caterpillar=cat)
+    check_case(case, _class_engine(case))
+
+
+def test_class_sweep_repetitive_alignment():
+    """Few distinct states per column (most subtrees repeat): long
+    aggregation segments crossing many 64-position tiles."""
+    rng = np.random.default_rng(70)
+    base = cases.random_case(70, S=48, P=5000, C=4, model="GTR")
+    codes = np.where(rng.random((48, 5000)) < 0.9, 1, rng.choice([1, 2, 4, 8, 15], size=(48, 5000)))
+    codes = codes.astype(np.uint8)
+    case = cases.Case("rep", codes, base.weights, base.peel0, True, "GTR", 4, base.blens, base.freqs,
+                      base.rates, base.rs, base.ps)
+    eng = _class_engine(case)
+    assert eng.class_info()["spans"] > 0
+    check_case(case, eng)
+
+
+def test_class_sweep_duplicate_columns_share_a_root_class():
+    """Patterns that differ only in raw symbols map to the same tip codes
+    (e.g. N and -): they share a root class whose weight is the sum; every
+    pattern still gets its own site log-likelihood."""
+    base = cases.random_case(71, S=10, P=80, C=2, model="HKY")
+    codes = np.concatenate([base.tipcodes, base.tipcodes[:, :20]], axis=1)
+    w = np.concatenate([base.weights, np.arange(1, 21, dtype=np.float64)])
+    case = cases.Case("dup", codes, w, base.peel0, True, "HKY", 2, base.blens, base.freqs, base.rates,
+                      base.rs, base.ps)
+    eng = _class_engine(case)
+    assert eng.class_info()["root_classes"] == 80
+    check_case(case, eng)
+
+
+def test_class_sweep_batched_draws_match_single():
+    base = cases.hcv_case()
+    rng = np.random.default_rng(3)
+    n = 5
+    eng = _class_engine(base, max_draws=n)
+    blens = base.blens[None, :] * rng.uniform(0.5, 1.5, (n, 1))
+    mvs = np.stack([cases.models.model_vector(base.freqs, base.rates * rng.uniform(0.8, 1.2, 6), base.rs,
+                                              base.ps) for _ in range(n)])
+    res = eng.evaluate_batch(blens, mvs, site_ll=True)
+    for k in range(n):
+        c = cases.Case("d%d" % k, base.tipcodes, base.weights, base.peel0, True, "GTR", 4, blens[k], base.freqs,
+                       mvs[k][4:10], base.rs, base.ps)
+        check_case(c, eng, res[k])
+
+
+def test_class_sweep_deterministic_and_agrees_with_pattern_sweep():
+    case = cases.random_case(72, S=64, P=2000, C=4, model="GTR")
+    eng = _class_engine(case)
+    a = eng.evaluate(case.blens, case.model_vec(), site_ll=True)
+    b = eng.evaluate(case.blens, case.model_vec(), site_ll=True)
+    assert a.loglik == b.loglik
+    assert np.array_equal(a.dLdP, b.dLdP) and np.array_equal(a.site_ll, b.site_ll)
+    eng.set_engine("pattern")
+    assert eng.engine() == "pattern"
+    c = eng.evaluate(case.blens, case.model_vec(), site_ll=True)
+    np.testing.assert_allclose(a.site_ll, c.site_ll, rtol=RTOL_LL, atol=1e-12)
+    _close(a.dLdP, c.dLdP, RTOL_G, "dLdP")
+
+
+def test_class_sweep_synthetic_200k_vs_c_port():
+    """The synthetic workload at 200k sites (121k patterns): the automatic
+    choice is the class sweep; against the OpenMP C port."""
+    import os
+    from oracle import cpu
+    from phylostan_amd import synthetic
+    from phylostan_amd.engine import EvalResult
+    pd, prm = synthetic.simulate(n_sites=200_000)
+    case = cases.Case("syn200k", pd.tipcodes, pd.weights, pd.peel0, True, "GTR", 4, prm["blens"], prm["freqs"],
+                      prm["rates"], prm["rs"], prm["ps"])
+    eng = _engine(case)
+    assert eng.engine() == "class"
+    res = eng.evaluate(case.blens, case.model_vec(), site_ll=True)
+    nt = max(1, min(16, os.cpu_count() or 1))
+    out, sl = cpu.evaluate(case.tipcodes, case.weights, case.peel0, True, 2, case.model_vec(), case.blens, 4,
+                           site_ll=True, nthreads=nt)
+    ref = EvalResult(out, eng.B, 4, sl)
+    np.testing.assert_allclose(res.site_ll, ref.site_ll, rtol=RTOL_LL, atol=1e-12)
+    assert abs(res.loglik - ref.loglik) <= RTOL_LL * abs(ref.loglik)
+    _close(res.dLdP, ref.dLdP, RTOL_G, "dLdP")
+    _close(res.grad_blens, ref.grad_blens, RTOL_G, "grad_blens")
+    _close(res.grad_rs, ref.grad_rs, RTOL_G, "grad_rs")
+    _close(res.grad_ps, ref.grad_ps, RTOL_G, "grad_ps")
+    _close(res.grad_freq_root, ref.grad_freq_root, RTOL_G, "grad_freq_root")

@@ -25,34 +25,51 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
 
-def run_pass(counter, out_dir, bench_args):
+CLASS_KERNELS = ("cls_fwd_kernel", "cls_root_ll_kernel", "cls_root_rev_kernel", "cls_red_kernel",
+                 "cls_fix_kernel", "cls_rev_kernel")
+
+
+def run_pass(counter, out_dir, bench_args, engine):
+    """Average per launch of the timed region: the sweep_kernel dispatch
+    (pattern sweep) or the sum of one evaluation's class-sweep dispatches
+    (class sweep; evaluations counted by cls_root_ll_kernel dispatches)."""
     cmd = ["rocprofv3", "--pmc", counter, "--kernel-trace", "-d", out_dir, "-o", "run",
            "--output-format", "csv", "--", sys.executable, os.path.join(ROOT, "bench.py")] + bench_args
     subprocess.run(cmd, check=True, stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL,
                    env=dict(os.environ, TMPDIR="/tmp"), timeout=900)
-    vals = []
+    total, n = 0.0, 0
     for f in glob.glob(os.path.join(out_dir, "**", "*counter_collection.csv"), recursive=True):
         for r in csv.DictReader(open(f)):
-            if "sweep_kernel" in r["Kernel_Name"] and r["Counter_Name"] == counter:
-                vals.append(float(r["Counter_Value"]))
-    if not vals:
-        raise RuntimeError("no %s samples for sweep_kernel" % counter)
-    return sum(vals) / len(vals), len(vals)
+            if r["Counter_Name"] != counter:
+                continue
+            name = r["Kernel_Name"]
+            if engine == "class":
+                if any(k in name for k in CLASS_KERNELS):
+                    total += float(r["Counter_Value"])
+                    n += "cls_root_ll_kernel" in name
+            elif "sweep_kernel" in name:
+                total += float(r["Counter_Value"])
+                n += 1
+    if not n:
+        raise RuntimeError("no %s samples for the %s sweep" % (counter, engine))
+    return total / n, n
 
 
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--workload", default="fluA")
     ap.add_argument("--draws", type=int, default=None)
+    ap.add_argument("--engine", choices=["pattern", "class"], default="pattern")
     ap.add_argument("--out", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
     ap.add_argument("--scratch", default=os.path.join(ROOT, "gpurun_out", "pmc"))
     args = ap.parse_args()
     from bench import kernel_source_hash
     draws = args.draws or (8192 if args.workload == "fluA" else 1)
     bench_args = ["--workload", args.workload, "--draws", str(draws), "--steps", "3", "--warmup", "1",
-                  "--no-cpu-baseline"]
-    fetch, nf = run_pass("FETCH_SIZE", os.path.join(args.scratch, args.workload + "_fetch"), bench_args)
-    write, nw = run_pass("WRITE_SIZE", os.path.join(args.scratch, args.workload + "_write"), bench_args)
+                  "--no-cpu-baseline", "--engine", args.engine]
+    tag = "%s_%s" % (args.workload, args.engine)
+    fetch, nf = run_pass("FETCH_SIZE", os.path.join(args.scratch, tag + "_fetch"), bench_args, args.engine)
+    write, nw = run_pass("WRITE_SIZE", os.path.join(args.scratch, tag + "_write"), bench_args, args.engine)
     traffic = (2.0 * fetch + write) * 1024.0
     rec = {}
     if os.path.exists(args.out):
@@ -62,7 +79,7 @@ def main():
             rec = {}
     if rec.get("kernel_source") != kernel_source_hash():
         rec = {"kernel_source": kernel_source_hash(), "per_launch_bytes": {}, "raw": {}}
-    key = "%s:%d" % (args.workload, draws)
+    key = "%s:%d:%s" % (args.workload, draws, args.engine)
     rec["per_launch_bytes"][key] = traffic
     rec["raw"][key] = {"FETCH_SIZE_KB": fetch, "WRITE_SIZE_KB": write, "dispatches": [nf, nw],
                        "formula": "(2*FETCH_SIZE + WRITE_SIZE) * 1024 (gfx950 FETCH_SIZE half-count correction)"}
