@@ -397,8 +397,11 @@ __device__ __forceinline__ V4 tipvec_b(unsigned b, unsigned long long extra) {
 // Register budget: K=2 targets two waves per SIMD (<= 256 VGPRs), K=1 four.
 // DL: the deep stack lives in LDS (no VMEM traffic or prefetch for it),
 // else in the per-workgroup global region behind a buffer descriptor.
+#ifndef PHY_WPE2
+#define PHY_WPE2 2  // waves per SIMD the K=2 kernel is register-budgeted for
+#endif
 template <int MAXT, int K, bool DL>
-__global__ void __launch_bounds__(MAXT) __attribute__((amdgpu_waves_per_eu(K == 2 ? 2 : 4)))
+__global__ void __launch_bounds__(MAXT) __attribute__((amdgpu_waves_per_eu(K == 2 ? PHY_WPE2 : 4)))
     sweep_kernel(SweepArgs a, const int* __restrict__ prog) {
   extern __shared__ __attribute__((aligned(16))) unsigned char lds_raw[];
   const int lane = threadIdx.x & (WAVE - 1);
@@ -1247,19 +1250,24 @@ __global__ void __launch_bounds__(256) finalize_kernel(FinArgs a) {
     const int lane = threadIdx.x & (WAVE - 1);
     const int nq = 2 + C + 4;  // ll, dps_0..C-1, dfreq_0..3 (+1 spare)
     for (int q = threadIdx.x / WAVE; q < nq - 1; q += blockDim.x / WAVE) {
-      double acc = 0.0;
-      for (int w = lane; w < a.gx; w += WAVE) {
+      // four slots in flight per lane (four accumulators, fixed combine order)
+      auto slot_val = [&](int w) -> double {
         const double* ss = a.sslot + (wg0 + w) * C * 8;
-        if (q == 0) {
-          acc += ss[0];
-        } else if (q <= C) {
-          acc += ss[(q - 1) * 8 + 1];
-        } else {
-          double t = 0.0;
-          for (int c = 0; c < C; ++c) t += ss[c * 8 + 2 + (q - 1 - C)];
-          acc += t;
+        if (q == 0) return ss[0];
+        if (q <= C) return ss[(q - 1) * 8 + 1];
+        double t = 0.0;
+        for (int c = 0; c < C; ++c) t += ss[c * 8 + 2 + (q - 1 - C)];
+        return t;
+      };
+      double acc4[4] = {0.0, 0.0, 0.0, 0.0};
+      for (int w0 = lane; w0 < a.gx; w0 += 4 * WAVE) {
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const int w = w0 + u * WAVE;
+          acc4[u] += (w < a.gx) ? slot_val(w) : 0.0;
         }
       }
+      double acc = (acc4[0] + acc4[1]) + (acc4[2] + acc4[3]);
       acc = wave_sum(acc);
       if (lane == 0) {
         if (q == 0)
@@ -1584,7 +1592,7 @@ constexpr size_t LDS_CAP = 160 * 1024;
 constexpr int MIN_CAP = 24;  // an occupancy level is taken only if chunks stay this large
 
 int nblk_for(int P, int K) { return (P + WAVE * K - 1) / (WAVE * K); }
-int waves_per_simd(int K) { return K == 2 ? 2 : 4; }  // the kernel's register budget
+int waves_per_simd(int K) { return K == 2 ? PHY_WPE2 : 4; }  // the kernel's register budget
 
 // Columns per lane, matrices per LDS chunk and the chunk boundaries over the
 // program.  Occupancy is bounded by registers (two waves per SIMD for K=2,
@@ -1789,7 +1797,7 @@ int launch_class(phy_ctx* ctx, int n, const double* d_blens, const double* d_mod
   }
   HIP_TRY(hipGetLastError());
   if (ctx->timing) HIP_TRY(hipEventRecord(e1, st));
-  hipLaunchKernelGGL(cls_gsum_kernel, dim3(B, dcn), dim3(256), 0, st, (const double*)e->d_gpart,
+  hipLaunchKernelGGL(cls_gsum_kernel, dim3(B, dcn), dim3(1024), 0, st, (const double*)e->d_gpart,
                      (const int*)e->d_gbase, (const int*)e->d_gcount, d_out, B, C, std::max(e->ngs, 1),
                      phy_output_len(ctx));
   if (d_site)
