@@ -42,12 +42,18 @@
  *             (1,kappa,1,1,kappa,1), generate_script.py:799-802; JC69 ignores)
  *     [10..10+C)     rs  (category rates)
  *     [10+C..10+2C)  ps  (category weights)
- *   Per-draw output vector, length phy_output_len() = 1 + B + 2C + 4 + 16*C*B:
+ *   Per-draw output vector, length phy_output_len() = 1 + B + 2C + 14 + 16*C*B
+ *   (1 + B + 2C + 14 when compact, phy_set_output):
  *     [0]                 log-likelihood  sum_i w_i log L_i
  *     [1 .. 1+B)          dlogL/dblens
  *     [1+B .. 1+B+C)      dlogL/drs
  *     [1+B+C .. 1+B+2C)   dlogL/dps
  *     [1+B+2C .. +4)      dlogL/dfreqs, explicit root term only
+ *     [1+B+2C+4 .. +6)    dlogL/d exchangeabilities AC AG AT CG CT GT through
+ *                         the normalised Q and its eigendecomposition
+ *                         (generate_script.py:839-892; HKY: dlogL/dkappa is
+ *                         the AG + CT entries; zeros for JC69)
+ *     [1+B+2C+10 .. +4)   dlogL/dfreqs, total (through Q plus the root term)
  *     [PHY_OUT_G(B,C) ..) dlogL/dP[c][b][4][4] (row-major P[j][k]); index
  *                         c*B + b is Stan's pmats[b + c*bcount]
  */
@@ -73,7 +79,7 @@ enum {
 };
 
 #define PHY_MODEL_LEN(C) (10 + 2 * (C))
-#define PHY_OUT_G(B, C) (1 + (B) + 2 * (C) + 4)
+#define PHY_OUT_G(B, C) (1 + (B) + 2 * (C) + 14)
 
 /* Build a context: copies the static data (tips, weights, topology) to the
  * device, derives the kernel traversal program and allocates every work
@@ -163,6 +169,12 @@ int phy_deep_stack_in_lds(const phy_ctx* ctx);
  * not store. */
 int phy_set_recompute(phy_ctx* ctx, int on);
 int phy_recomputed_partials(const phy_ctx* ctx);
+
+/* Output rows: compact = 1 drops the dL/dP block (rows end after the
+ * model-parameter gradients: what a sampler consumes, 1 + B + 2C + 14
+ * doubles per draw instead of + 16CB more); 0 = full rows (default).
+ * phy_output_len follows. */
+int phy_set_output(phy_ctx* ctx, int compact);
 
 /* Engine: 1 = pattern sweep (one lane per pattern column), 2 = class sweep
  * (site repeats: the forward pass once per distinct tip-state tuple of each

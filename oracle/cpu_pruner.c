@@ -153,7 +153,10 @@ int oracle_eval(int S, int P, int C, int rooted, int kind, const uint8_t* tipcod
                 double* out, double* site_ll, int nthreads) {
   const int B = rooted ? 2 * S - 2 : 2 * S - 3;
   const int N = 2 * S - 1;
-  const int og = 1 + B + 2 * C + 4;
+  /* [ll, grad_blens, grad_rs, grad_ps, grad_freq_root(4), grad_rates(6),
+   * grad_freqs(4), dL/dP]: the 10 model-parameter slots are left zero here
+   * and filled by oracle/cpu.py with the host chain rule */
+  const int og = 1 + B + 2 * C + 4 + 10;
   const double* f = model;
   const double* rs = model + 10;
   const double* ps = model + 10 + C;

@@ -125,8 +125,8 @@ __device__ __forceinline__ Step ld_step(const int* __restrict__ prog, int s) {
   return t;
 }
 // Per-draw eigensystem record: P(t) = m1 diag(exp(lam t)) m2, plus Q.
-constexpr int EIG_LEN = 56;  // m1[16] lam[4] m2[16] Q[16] (+pad)
-constexpr int EIG_M1 = 0, EIG_LAM = 16, EIG_M2 = 20, EIG_Q = 36;
+constexpr int EIG_LEN = 56;  // m1[16] lam[4] m2[16] Q[16] s (+pad)
+constexpr int EIG_M1 = 0, EIG_LAM = 16, EIG_M2 = 20, EIG_Q = 36, EIG_S = 52;
 
 thread_local std::string g_err;
 
@@ -271,6 +271,8 @@ struct SweepArgs {
   unsigned long long extra;  // tip masks of record vectors 4..R-1, 4 bits each
   int fin;  // g_direct and the finalize fits in LDS: the sweep writes the whole output row
   const double* blens;  // [draw][B] (fin)
+  double* grows;        // dL/dP rows of draw d at grows + d * grows_stride (in `out`, or scratch when compact)
+  long long grows_stride;
 };
 
 // LDS carve (16-B aligned pieces), K columns per lane:
@@ -904,7 +906,7 @@ __global__ void __launch_bounds__(MAXT) __attribute__((amdgpu_waves_per_eu(K == 
     double* scalL = mats0 + (size_t)C * a.B;
     if (a.fin) __syncthreads();
     const double* Qd = a.eig + (size_t)draw * EIG_LEN + EIG_Q;
-    double* gout = a.out + (size_t)draw * a.outlen + 1 + a.B + 2 * C + 4;
+    double* gout = a.grows + (size_t)draw * a.grows_stride;
     double* inner_d = a.inner + (size_t)draw * C * a.B;
     // k = lane (mod 64): every item of this lane has the same entry e16 =
     // (j, kk), so the Q row is loaded once
@@ -1081,6 +1083,7 @@ __global__ void __launch_bounds__(64) eig_kernel(PmatArgs a) {
       q[j][k] /= s;  // :868
       out[EIG_Q + j * 4 + k] = q[j][k];
     }
+  out[EIG_S] = s;  // the normaliser, for the Q-parameter chain rule
 #pragma unroll
   for (int j = 0; j < 4; ++j)  // A = Pi^1/2 Q Pi^-1/2, symmetrised (:870)
 #pragma unroll
@@ -1188,6 +1191,9 @@ struct FinArgs {
   const double* inner;  // [draw][C][B] <G, Q P> from the sweep when g_direct
   double* out;          // [draw][outlen]
   int C, B, nmat, gx, outlen, g_direct, R;
+  double* grows;        // dL/dP rows (see SweepArgs)
+  long long grows_stride;
+  int kind;
 };
 
 // dL/dP of a draw spread over several workgroups: out[draw][og + (c*B+b)*16
@@ -1223,7 +1229,7 @@ __global__ void __launch_bounds__(256) gsum_kernel(FinArgs a) {
   __syncthreads();
   if (grp == 0 && idx < ng) {
     const double s = ((part[0][threadIdx.x] + part[1][threadIdx.x]) + part[2][threadIdx.x]) + part[3][threadIdx.x];
-    a.out[(size_t)draw * a.outlen + 1 + B + 2 * C + 4 + idx] = s;
+    a.grows[(size_t)draw * a.grows_stride + idx] = s;
   }
 }
 
@@ -1240,7 +1246,6 @@ __global__ void __launch_bounds__(256) finalize_kernel(FinArgs a) {
   double* Q = fsh + (size_t)C * B;
   double* out = a.out + (size_t)draw * a.outlen;
   const size_t wg0 = (size_t)draw * a.gx;
-  const int og = 1 + B + 2 * C + 4;
   if (threadIdx.x < 16) Q[threadIdx.x] = a.eig[(size_t)draw * EIG_LEN + EIG_Q + threadIdx.x];
   {
     // scalar partials per slot: [c][8] = ll (c = 0 only), dps_c, dfreq[4];
@@ -1288,7 +1293,7 @@ __global__ void __launch_bounds__(256) finalize_kernel(FinArgs a) {
       continue;
     }
     const int c = idx / B, b = idx - c * B;
-    const double* g = out + og + (size_t)idx * 16;
+    const double* g = a.grows + (size_t)draw * a.grows_stride + (size_t)idx * 16;
     const double* P = pm + ((size_t)c * a.nmat + a.gpos[b]) * rec;  // column-major
     double gv[16], pv[16];
 #pragma unroll
@@ -1323,6 +1328,141 @@ __global__ void __launch_bounds__(256) finalize_kernel(FinArgs a) {
   }
 }
 
+// dlogL / d(exchangeabilities[6], freqs[4]) through the eigendecomposition:
+// the device form of models.q_param_gradients_batch (Q = V diag(lam) V^-1,
+// V = m1 = Pi^-1/2 U, V^-1 = m2 = U^T Pi^1/2, t = r_c b):
+//   H_cb = V^T G_cb V^-T,  Phi_cb[k][l] = (e^{lam_k t} - e^{lam_l t}) / (lam_k - lam_l)
+//   (t e^{lam_k t} on ties),  M = sum_cb H_cb .* Phi_cb,  W = V^-T M V^T,
+//   qw = <Q, W>,  s = the normaliser of Q (generate_script.py:862-868);
+//   rate (i,j): (f_j W_ij + f_i W_ji - f_j W_ii - f_i W_jj - 2 f_i f_j qw) / s
+//   freq m:     (sum_{j != m} R_jm (W_jm - W_jj) - qw sum_{j != m} 2 R_mj f_j) / s
+//               + the explicit root term.
+// One workgroup per draw; per-thread partial M over (c, b), then a
+// fixed-order sum: deterministic.  JC69 has no Q parameters: zeros.
+__global__ void __launch_bounds__(256) qgrad_kernel(FinArgs a) {
+  __shared__ double part[256][17];
+  const int draw = blockIdx.x, tid = threadIdx.x;
+  const int C = a.C, B = a.B;
+  double* out = a.out + (size_t)draw * a.outlen;
+  const int o = 1 + B + 2 * C;
+  if (a.kind == PHY_JC69) {
+    if (tid < 10) out[o + 4 + tid] = 0.0;
+    return;
+  }
+  const double* e = a.eig + (size_t)draw * EIG_LEN;
+  double V[16], Vi[16], lam[4];
+#pragma unroll
+  for (int k = 0; k < 16; ++k) {
+    V[k] = e[EIG_M1 + k];
+    Vi[k] = e[EIG_M2 + k];
+  }
+#pragma unroll
+  for (int k = 0; k < 4; ++k) lam[k] = e[EIG_LAM + k];
+  const double* mdl = a.model + (size_t)draw * (10 + 2 * C);
+  const double* bl = a.blens + (size_t)draw * B;
+  const double* rows = a.grows + (size_t)draw * a.grows_stride;
+  // 1 / (lam_k - lam_l) once per draw (0 marks a tie: t e^{lam_k t} there)
+  double rinv[16];
+#pragma unroll
+  for (int k = 0; k < 4; ++k)
+#pragma unroll
+    for (int l = 0; l < 4; ++l) {
+      const double d = lam[k] - lam[l];
+      rinv[k * 4 + l] = fabs(d) < 1e-12 * fmax(1.0, fabs(lam[k])) ? 0.0 : 1.0 / d;
+    }
+  double m[16];
+#pragma unroll
+  for (int k = 0; k < 16; ++k) m[k] = 0.0;
+  for (int idx = tid; idx < C * B; idx += blockDim.x) {
+    const int c = idx / B, b = idx - c * B;
+    const double t = mdl[10 + c] * bl[b];
+    double G[16];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) G[k] = rows[(size_t)idx * 16 + k];
+    double T[16];  // V^T G
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        double acc = 0.0;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) acc = fma(V[i * 4 + k], G[i * 4 + j], acc);
+        T[k * 4 + j] = acc;
+      }
+    double E[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) E[k] = exp(lam[k] * t);
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+#pragma unroll
+      for (int l = 0; l < 4; ++l) {
+        double h = 0.0;  // (V^T G V^-T)[k][l]
+#pragma unroll
+        for (int j = 0; j < 4; ++j) h = fma(T[k * 4 + j], Vi[l * 4 + j], h);
+        const double ri = rinv[k * 4 + l];
+        const double phi = ri == 0.0 ? t * E[k] : (E[k] - E[l]) * ri;
+        m[k * 4 + l] = fma(h, phi, m[k * 4 + l]);
+      }
+  }
+#pragma unroll
+  for (int k = 0; k < 16; ++k) part[tid][k] = m[k];
+  __syncthreads();
+  if (tid < 16) {
+    double acc = 0.0;
+    for (int q = 0; q < (int)blockDim.x; ++q) acc += part[q][tid];
+    part[0][tid] = acc;  // row 0 is read only by thread tid itself above
+  }
+  __syncthreads();
+  if (tid != 0) return;
+  double M[16], W[16];
+#pragma unroll
+  for (int k = 0; k < 16; ++k) M[k] = part[0][k];
+  // W = V^-T M V^T: W[i][j] = sum_kl Vi[k][i] M[k][l] V[j][l]
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      double acc = 0.0;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        double ml = 0.0;
+#pragma unroll
+        for (int l = 0; l < 4; ++l) ml = fma(M[k * 4 + l], V[j * 4 + l], ml);
+        acc = fma(Vi[k * 4 + i], ml, acc);
+      }
+      W[i * 4 + j] = acc;
+    }
+  const double* Q = e + EIG_Q;
+  const double s = e[EIG_S];
+  double qw = 0.0;
+#pragma unroll
+  for (int k = 0; k < 16; ++k) qw = fma(Q[k], W[k], qw);
+  const double f[4] = {mdl[0], mdl[1], mdl[2], mdl[3]};
+  const double* r = mdl + 4;  // AC AG AT CG CT GT
+  const int pi_[6] = {0, 0, 0, 1, 1, 2}, pj_[6] = {1, 2, 3, 2, 3, 3};
+  double Rm[16];
+#pragma unroll
+  for (int k = 0; k < 16; ++k) Rm[k] = 0.0;
+#pragma unroll
+  for (int k = 0; k < 6; ++k) {
+    const int i = pi_[k], j = pj_[k];
+    Rm[i * 4 + j] = Rm[j * 4 + i] = r[k];
+    const double dq = f[j] * W[i * 4 + j] + f[i] * W[j * 4 + i] - f[j] * W[i * 4 + i] - f[i] * W[j * 4 + j];
+    out[o + 4 + k] = (dq - 2.0 * f[i] * f[j] * qw) / s;
+  }
+#pragma unroll
+  for (int mm = 0; mm < 4; ++mm) {
+    double dq = 0.0, ds = 0.0;
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      if (j != mm) {
+        dq += Rm[j * 4 + mm] * (W[j * 4 + mm] - W[j * 4 + j]);
+        ds += 2.0 * Rm[mm * 4 + j] * f[j];
+      }
+    out[o + 10 + mm] = (dq - ds * qw) / s + out[o + mm];
+  }
+}
+
 }  // namespace
 
 // ---------------------------------------------------------------------------
@@ -1352,6 +1492,8 @@ struct phy_ctx {
   // class_engine.inc); engine_pref 0 = automatic, 1 = pattern, 2 = class
   int engine = 0, engine_pref = 0;
   ClassEngine* ce = nullptr;
+  int compact = 0;             // output rows without the dL/dP block (phy_set_output)
+  double* d_grows = nullptr;   // dL/dP rows when compact: [max_draws][16 C B]
   std::vector<uint8_t> h_tips;  // host copies of the static data (the class plan is built on demand)
   std::vector<double> h_w;
   std::vector<int32_t> h_peel;
@@ -1390,7 +1532,7 @@ void free_ctx(phy_ctx* c) {
   (void)hipSetDevice(c->device);
   void* ptrs[] = {c->d_tips,  c->d_w,     c->d_prog,    c->d_gpos,    c->d_mat_branch, c->d_pmat,
                   c->d_eig,   c->d_inner, c->d_model,   c->d_blens,   c->d_out,        c->d_site,
-                  c->d_scratch, c->d_dstk, c->d_gslot,  c->d_sslot};
+                  c->d_scratch, c->d_dstk, c->d_gslot,  c->d_sslot, c->d_grows};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   for (hipEvent_t e : c->ev) (void)hipEventDestroy(e);
@@ -1763,7 +1905,7 @@ int timing_begin(phy_ctx* ctx, hipStream_t st, hipEvent_t* e0, hipEvent_t* e1) {
 // then the ordered dL/dP sums and the shared finalize.  The timed region
 // (phy_timing_*) spans the forward through the last reverse level.
 int launch_class(phy_ctx* ctx, int n, const double* d_blens, const double* d_model, double* d_out,
-                 double* d_site, hipStream_t st) {
+                 double* d_site, hipStream_t st, double* grows, long long gstride) {
   ClassEngine* e = ctx->ce;
   const int C = ctx->C, B = ctx->B;
   if ((long)n * C > 65535) return fail(PHY_ERANGE, "class sweep: n_draws * C must be <= 65535");
@@ -1798,17 +1940,20 @@ int launch_class(phy_ctx* ctx, int n, const double* d_blens, const double* d_mod
   HIP_TRY(hipGetLastError());
   if (ctx->timing) HIP_TRY(hipEventRecord(e1, st));
   hipLaunchKernelGGL(cls_gsum_kernel, dim3(B, dcn), dim3(1024), 0, st, (const double*)e->d_gpart,
-                     (const int*)e->d_gbase, (const int*)e->d_gcount, d_out, B, C, std::max(e->ngs, 1),
-                     phy_output_len(ctx));
+                     (const int*)e->d_gbase, (const int*)e->d_gcount, grows, gstride, B, C, std::max(e->ngs, 1));
   if (d_site)
     hipLaunchKernelGGL(cls_site_kernel, dim3((ctx->P + 255) / 256, n), dim3(256), 0, st,
                        (const double*)e->d_sitecls, (const int*)e->d_pat_root, d_site, ctx->P, e->nroot);
   FinArgs fa{ctx->d_gslot, e->d_sslot, ctx->d_pmat, ctx->d_eig, d_blens, d_model, ctx->d_gpos, ctx->d_inner, d_out,
-             C,            B,          ctx->nmat,   e->nrootch,  phy_output_len(ctx), 0, ctx->R};
+             C,            B,          ctx->nmat,   e->nrootch,  phy_output_len(ctx), 0, ctx->R, grows, gstride,
+             ctx->kind};
   hipLaunchKernelGGL(finalize_kernel, dim3(n), dim3(256), ((size_t)C * B + 16) * sizeof(double), st, fa);
   HIP_TRY(hipGetLastError());
   return PHY_OK;
 }
+
+int launch_pattern(phy_ctx* ctx, int n, const double* d_blens, const double* d_model, double* d_out,
+                   double* d_site, hipStream_t st, double* grows, long long gstride);
 
 int launch(phy_ctx* ctx, int n, const double* d_blens, const double* d_model, double* d_out,
            double* d_site, hipStream_t st) {
@@ -1822,7 +1967,23 @@ int launch(phy_ctx* ctx, int n, const double* d_blens, const double* d_model, do
                        (size_t)PMAT_WAVE_RECS * ctx->R * 4 * sizeof(double), st, pa);
     HIP_TRY(hipGetLastError());
   }
-  if (ctx->engine == 1) return launch_class(ctx, n, d_blens, d_model, d_out, d_site, st);
+  double* grows = ctx->compact ? ctx->d_grows : d_out + PHY_OUT_G(B, C);
+  const long long gstride = ctx->compact ? (long long)16 * C * B : (long long)phy_output_len(ctx);
+  int rc0 = ctx->engine == 1 ? launch_class(ctx, n, d_blens, d_model, d_out, d_site, st, grows, gstride)
+                             : launch_pattern(ctx, n, d_blens, d_model, d_out, d_site, st, grows, gstride);
+  if (rc0) return rc0;
+  FinArgs qa{ctx->d_gslot, ctx->d_sslot, ctx->d_pmat, ctx->d_eig, d_blens, d_model, ctx->d_gpos, ctx->d_inner, d_out,
+             C,            B,            ctx->nmat,   1,           phy_output_len(ctx), 0, ctx->R, grows, gstride,
+             ctx->kind};
+  hipLaunchKernelGGL(qgrad_kernel, dim3(n), dim3(256), 0, st, qa);
+  HIP_TRY(hipGetLastError());
+  return PHY_OK;
+}
+
+// The pattern sweep (sweep_kernel) and its dL/dP sums / finalize.
+int launch_pattern(phy_ctx* ctx, int n, const double* d_blens, const double* d_model, double* d_out,
+                   double* d_site, hipStream_t st, double* grows, long long gstride) {
+  const int C = ctx->C, B = ctx->B;
   // persistent workgroups: the explicit budget, else exactly what is resident
   const int budget = ctx->wg_budget > 0 ? ctx->wg_budget : ctx->wg_resident;
   const int gx = std::max(1, std::min(ctx->nblk, (budget + n - 1) / n));
@@ -1836,7 +1997,7 @@ int launch(phy_ctx* ctx, int n, const double* d_blens, const double* d_model, do
                ctx->d_gslot, ctx->d_sslot, d_site,       d_out,        ctx->d_mat_branch, ctx->d_eig,
                ctx->d_inner, ctx->S,       ctx->P,       ctx->Ppad,    C,              ctx->nsteps,
                ctx->nslots,  ctx->ndeep,   ctx->ndl,     ctx->nblk,    ctx->nmat,    ctx->R,         ctx->cap_m,
-               B,            phy_output_len(ctx), g_direct, ctx->extra, fin, d_blens};
+               B,            phy_output_len(ctx), g_direct, ctx->extra, fin, d_blens, grows, gstride};
   hipEvent_t e0 = nullptr, e1 = nullptr;
   if (ctx->timing) {
     int rc = timing_begin(ctx, st, &e0, &e1);
@@ -1856,7 +2017,8 @@ int launch(phy_ctx* ctx, int n, const double* d_blens, const double* d_model, do
   HIP_TRY(hipGetLastError());
   if (ctx->timing) HIP_TRY(hipEventRecord(e1, st));
   FinArgs fa{ctx->d_gslot, ctx->d_sslot, ctx->d_pmat, ctx->d_eig, d_blens, d_model, ctx->d_gpos, ctx->d_inner, d_out,
-             C,            B,            ctx->nmat,   gx,          phy_output_len(ctx), g_direct, ctx->R};
+             C,            B,            ctx->nmat,   gx,          phy_output_len(ctx), g_direct, ctx->R, grows, gstride,
+             ctx->kind};
   if (!g_direct) {
     hipLaunchKernelGGL(gsum_kernel, dim3((C * B * 16 + 63) / 64, n), dim3(256), 0, st, fa);
     HIP_TRY(hipGetLastError());
@@ -2065,7 +2227,20 @@ int phy_destroy(phy_ctx* ctx) {
 int phy_num_branches(const phy_ctx* ctx) { return ctx ? ctx->B : -1; }
 
 int phy_output_len(const phy_ctx* ctx) {
-  return ctx ? 1 + ctx->B + 2 * ctx->C + 4 + 16 * ctx->C * ctx->B : -1;
+  if (!ctx) return -1;
+  return PHY_OUT_G(ctx->B, ctx->C) + (ctx->compact ? 0 : 16 * ctx->C * ctx->B);
+}
+
+int phy_set_output(phy_ctx* ctx, int compact) {
+  if (!ctx) return fail(PHY_EINVAL, "NULL ctx");
+  HIP_TRY(hipSetDevice(ctx->device));
+  HIP_TRY(hipStreamSynchronize(ctx->stream));
+  if (compact && !ctx->d_grows) {
+    int rc = dalloc(&ctx->d_grows, (size_t)ctx->max_draws * 16 * ctx->C * ctx->B);
+    if (rc) return rc;
+  }
+  ctx->compact = compact ? 1 : 0;
+  return PHY_OK;
 }
 
 int phy_program_info(const phy_ctx* ctx, int* nsteps, int* nslots, int* depth, int* nblocks) {

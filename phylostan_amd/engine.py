@@ -27,17 +27,20 @@ from . import models
 class EvalResult:
     """Unpacked output vector of one draw (layout: include/phylo_hip.h)."""
 
-    __slots__ = ("loglik", "grad_blens", "grad_rs", "grad_ps", "grad_freq_root", "dLdP",
-                 "site_ll")
+    __slots__ = ("loglik", "grad_blens", "grad_rs", "grad_ps", "grad_freq_root", "grad_rates", "grad_freqs",
+                 "dLdP", "site_ll")
 
     def __init__(self, vec, B, C, site_ll=None):
-        og = 1 + B + 2 * C + 4
+        o = 1 + B + 2 * C
+        og = o + 4 + 10
         self.loglik = float(vec[0])
         self.grad_blens = vec[1:1 + B].copy()
         self.grad_rs = vec[1 + B:1 + B + C].copy()
-        self.grad_ps = vec[1 + B + C:1 + B + 2 * C].copy()
-        self.grad_freq_root = vec[1 + B + 2 * C:og].copy()
-        self.dLdP = vec[og:og + C * B * 16].reshape(C, B, 4, 4).copy()
+        self.grad_ps = vec[1 + B + C:o].copy()
+        self.grad_freq_root = vec[o:o + 4].copy()
+        self.grad_rates = vec[o + 4:o + 10].copy()   # d/d exchangeabilities AC AG AT CG CT GT
+        self.grad_freqs = vec[o + 10:og].copy()      # d/d freqs: through Q plus the root term
+        self.dLdP = vec[og:og + C * B * 16].reshape(C, B, 4, 4).copy() if len(vec) >= og + C * B * 16 else None
         self.site_ll = site_ll
 
     def as_dict(self):
@@ -177,6 +180,12 @@ class TreeLikelihood:
         out["deep_lds_entries"] = self.lib.phy_deep_stack_in_lds(self.ctx)
         out["recomputed"] = self.lib.phy_recomputed_partials(self.ctx)
         return out
+
+    def set_output(self, compact=False):
+        """compact: output rows stop after the model-parameter gradients (no
+        dL/dP block: 1 + B + 2C + 14 doubles per draw, what a sampler needs)."""
+        _lib.check(self.lib.phy_set_output(self.ctx, int(bool(compact))), "phy_set_output")
+        self.outlen = self.lib.phy_output_len(self.ctx)
 
     def set_engine(self, mode=0):
         """0 automatic, 1 pattern sweep, 2 class sweep (site repeats)."""

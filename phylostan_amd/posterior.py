@@ -140,6 +140,8 @@ class Posterior:
         self.spec = spec
         self.tree = tree
         self.lik = likelihood
+        if hasattr(likelihood, "set_output"):
+            likelihood.set_output(compact=True)  # the sampler needs no dL/dP block
         S = tree.S
         self.S = S
         self.C = spec.C
@@ -564,16 +566,16 @@ class Posterior:
         g_rs = np.stack([r.grad_rs if r is not None else zc for r in res])
         g_ps = np.stack([r.grad_ps if r is not None else zc for r in res])
         if sp.model != "JC69":
+            # the engine's chain rule through Q's eigendecomposition (include/phylo_hip.h)
             good = np.nonzero(~bad)[0]
             if len(good):
-                gr, gf = models.q_param_gradients_batch(
-                    np.stack([res[d].dLdP for d in good]), blens[good], rs[good], freqs[good], R[good],
-                    np.stack([res[d].grad_freq_root for d in good]))
+                gr = np.stack([res[d].grad_rates for d in good])
+                gf = np.stack([res[d].grad_freqs for d in good])
                 gx["freqs"][good] += gf
                 if sp.model == "GTR":
                     gx["rates"][good] += gr
                 else:
-                    gx["kappa"][good] += gr[:, 1] + gr[:, 4]  # kappa_gradient: AG and CT
+                    gx["kappa"][good] += gr[:, 1] + gr[:, 4]  # kappa enters AG and CT
         self._site_rates_backward(vals, g_rs, g_ps, gx, rs, ps)
         if self.clock:
             gspan = g_bl * mult

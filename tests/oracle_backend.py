@@ -9,6 +9,7 @@ from types import SimpleNamespace
 import numpy as np
 
 from oracle import numpy_pruner as npr
+from phylostan_amd import models
 
 
 class OracleLikelihood:
@@ -35,9 +36,13 @@ class OracleLikelihood:
             P, Q = npr.model_matrices(self.kind, freqs, q, b, rs)
             fr = freqs if self.kind != npr.JC69 else np.full(4, 0.25)
             r = npr.prune(self.tipcodes, self.weights, self.peel0, self.rooted, P, fr, ps, Q=Q, blens=b, rs=rs)
+            if self.kind == npr.JC69:
+                gr, gf = np.zeros(6), np.zeros(4)
+            else:  # the host chain rule (the engine does it on the device)
+                gr, gf = models.q_param_gradients(r["dLdP"], b, rs, freqs, rates, r["grad_freq_root"])
             out.append(SimpleNamespace(loglik=float(r["loglik"]), grad_blens=r["grad_blens"], grad_rs=r["grad_rs"],
                                        grad_ps=r["grad_ps"], grad_freq_root=r["grad_freq_root"], dLdP=r["dLdP"],
-                                       site_ll=r["site_ll"] if site_ll else None))
+                                       grad_rates=gr, grad_freqs=gf, site_ll=r["site_ll"] if site_ll else None))
         return out
 
     def evaluate(self, blens, model_vec, site_ll=False):

@@ -29,7 +29,7 @@ class OracleShardEngine:
         S = tipcodes.shape[0]
         self.B = 2 * S - 2 if rooted else 2 * S - 3
         self.C = C
-        self.outlen = 1 + self.B + 2 * C + 4 + 16 * C * self.B
+        self.outlen = 1 + self.B + 2 * C + 4 + 10 + 16 * C * self.B
 
     def evaluate_device(self, d_blens, d_model, d_out, d_site_ll=0, n_draws=1, stream=0):
         from oracle import cpu

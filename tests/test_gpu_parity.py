@@ -43,6 +43,14 @@ def check_case(case, eng=None, res=None):
     _close(res.grad_rs, ref["grad_rs"], RTOL_G, "grad_rs")
     _close(res.grad_ps, ref["grad_ps"], RTOL_G, "grad_ps")
     _close(res.grad_freq_root, ref["grad_freq_root"], RTOL_G, "grad_freq_root")
+    if case.model == "JC69":
+        assert not np.any(res.grad_rates) and not np.any(res.grad_freqs)
+    else:  # the device chain rule through Q vs the host one on the oracle's dL/dP
+        from phylostan_amd import models
+        gr, gf = models.q_param_gradients(ref["dLdP"], case.blens, case.rs, case.freqs, case.rates,
+                                          ref["grad_freq_root"])
+        _close(res.grad_rates, gr, 1e-8, "grad_rates")
+        _close(res.grad_freqs, gf, 1e-8, "grad_freqs")
     return res
 
 
@@ -346,3 +354,25 @@ def test_synthetic_full_size_vs_c_port():
     _close(res.grad_rs, ref.grad_rs, RTOL_G, "grad_rs")
     _close(res.grad_ps, ref.grad_ps, RTOL_G, "grad_ps")
     _close(res.grad_freq_root, ref.grad_freq_root, RTOL_G, "grad_freq_root")
+
+
+@pytest.mark.parametrize("engine", ["pattern", "class"])
+def test_compact_output_rows(engine):
+    """phy_set_output(compact): the rows stop after the model-parameter
+    gradients; every value equals the full row's bit for bit."""
+    case = cases.hcv_case()
+    eng = _engine(case, max_draws=3)
+    eng.set_engine(engine)
+    rng = np.random.default_rng(9)
+    bl = case.blens[None, :] * rng.uniform(0.8, 1.2, (3, 1))
+    mv = np.repeat(case.model_vec()[None], 3, axis=0)
+    full = eng.evaluate_batch(bl, mv)
+    n_full = eng.outlen
+    eng.set_output(compact=True)
+    assert eng.outlen == n_full - 16 * case.C * eng.B == 1 + eng.B + 2 * case.C + 14
+    comp = eng.evaluate_batch(bl, mv)
+    for a, b in zip(full, comp):
+        assert b.dLdP is None and a.loglik == b.loglik
+        for k in ("grad_blens", "grad_rs", "grad_ps", "grad_freq_root", "grad_rates", "grad_freqs"):
+            np.testing.assert_array_equal(getattr(a, k), getattr(b, k))
+    check_case(case, eng.__class__(case.tipcodes, case.weights, case.peel0, case.rooted, case.model, case.C))

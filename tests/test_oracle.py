@@ -159,7 +159,7 @@ def test_c_oracle_matches_numpy(make):
     out, sl = cpu.evaluate(case.tipcodes, case.weights, case.peel0, case.rooted, npr.MODEL_IDS[case.model],
                            case.model_vec(), case.blens, case.C, site_ll=True, nthreads=2)
     B = len(case.blens)
-    og = 1 + B + 2 * case.C + 4
+    og = 1 + B + 2 * case.C + 4 + 10
     np.testing.assert_allclose(sl, ref["site_ll"], rtol=1e-10, atol=1e-12)
     np.testing.assert_allclose(out[og:], ref["dLdP"].ravel(), rtol=1e-8, atol=1e-9 * np.abs(ref["dLdP"]).max())
     np.testing.assert_allclose(out[1:1 + B], ref["grad_blens"], rtol=1e-8, atol=1e-9 * np.abs(ref["grad_blens"]).max())
