@@ -141,16 +141,16 @@ def algorithmic_bytes(S, P, C, nslots, B, draws):
     return per_draw * draws
 
 
-def class_algorithmic_bytes(C, classes, stage, draws):
+def class_algorithmic_bytes(C, classes, stage, staged, draws):
     """HBM bytes of one class-sweep evaluation (DESIGN.md "Class sweep"):
     per category, every non-root subtree class's moved partial is written
-    once (forward) and its aggregated upper partial written (RED) and read
-    (REV) once -- 3 x 32 B per class; every contribution a parent class makes
-    to an internal child is gathered in the forward, gathered again and
-    stored in the reverse, and read by the segmented reduction -- 4 x 32 B
-    per staging element (``stage`` = sum over internal nodes of classes x
-    internal children, the root's included)."""
-    return 32 * C * (3 * classes + 4 * stage) * draws
+    once (forward) and its aggregated upper partial written and read once --
+    3 x 32 B per class; every contribution a parent class makes to an
+    internal child (``stage`` of them) needs that child's vector gathered in
+    the forward and again in the reverse -- 2 x 32 B; the ``staged`` ones
+    (secondary children) are also stored and read back by the segmented
+    reduction -- 2 x 32 B more (a primary child's are reduced in registers)."""
+    return 32 * C * (3 * classes + 2 * stage + 2 * staged) * draws
 
 
 def survey_bytes(S, P, C, draws):
@@ -418,7 +418,7 @@ def main():
         single = dict(evals_per_s=n1 / (tb - ta), us_per_eval=1e6 * (tb - ta) / n1)
 
     if info["engine"] == "class":
-        alg = class_algorithmic_bytes(C, info["class_classes"], info["class_stage"], draws)
+        alg = class_algorithmic_bytes(C, info["class_classes"], info["class_stage"], info["class_staged"], draws)
         kernel_name = "class sweep: cls_fwd/cls_root/cls_red/cls_fix/cls_rev kernels, forward through reverse"
     else:
         alg = algorithmic_bytes(S, P_local, C, info["nslots"] - info.get("recomputed", 0), B, draws)

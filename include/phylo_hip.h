@@ -190,11 +190,13 @@ int phy_engine(const phy_ctx* ctx);
 
 /* Class-plan facts (zeros when no plan is built): non-root subtree classes
  * (the class sweep's forward work per category), levels (the root's level),
- * root classes (distinct site patterns by tip state), staging elements (sum
- * over internal nodes of classes x internal children: the reverse's
- * contributions), reduction tiles and tile-crossing segments. */
+ * root classes (distinct site patterns by tip state), contributions (sum over
+ * internal nodes of classes x internal children: the reverse's aggregation
+ * inputs), the part of them staged through HBM (secondary children; a
+ * primary child's are reduced in registers), reduction tiles and
+ * tile-crossing segments. */
 int phy_class_info(const phy_ctx* ctx, long long* classes, int* levels, int* root_classes, long long* stage,
-                   int* tiles, int* spans);
+                   long long* staged, int* tiles, int* spans);
 
 #ifdef __cplusplus
 }

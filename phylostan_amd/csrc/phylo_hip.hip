@@ -1931,6 +1931,11 @@ int launch_class(phy_ctx* ctx, int n, const double* d_blens, const double* d_mod
       a.count = L.ntile;
       hipLaunchKernelGGL(cls_red_kernel, dim3((L.ntile + 3) / 4, dcn), dim3(256), 0, st, a);
     }
+    if (L.nspan) {
+      a.first = L.span0;
+      a.count = L.nspan;
+      hipLaunchKernelGGL(cls_fix_kernel, dim3((L.nspan + 3) / 4, dcn), dim3(256), 0, st, a);
+    }
     if (L.nchunk) {
       a.first = L.chunk0;
       a.count = L.nchunk;
@@ -2377,7 +2382,7 @@ int phy_set_engine(phy_ctx* ctx, int mode) {
 int phy_engine(const phy_ctx* ctx) { return ctx ? ctx->engine : -1; }
 
 int phy_class_info(const phy_ctx* ctx, long long* classes, int* levels, int* root_classes, long long* stage,
-                   int* tiles, int* spans) {
+                   long long* staged, int* tiles, int* spans) {
   if (!ctx) return fail(PHY_EINVAL, "NULL ctx");
   const ClassEngine* e = ctx->ce;
   long long ns = 0;
@@ -2389,6 +2394,7 @@ int phy_class_info(const phy_ctx* ctx, long long* classes, int* levels, int* roo
   if (levels) *levels = e ? e->levels : 0;
   if (root_classes) *root_classes = e ? e->nroot : 0;
   if (stage) *stage = ns;
+  if (staged) *staged = e ? e->stage_sec : 0;
   if (tiles) *tiles = e ? e->ntiles : 0;
   if (spans) *spans = nspan;
   return PHY_OK;

@@ -198,13 +198,13 @@ class TreeLikelihood:
         return ("pattern", "class")[self.lib.phy_engine(self.ctx)]
 
     def class_info(self):
-        ll = [ctypes.c_longlong() for _ in range(2)]
+        ll = [ctypes.c_longlong() for _ in range(3)]
         ii = [ctypes.c_int() for _ in range(4)]
         _lib.check(self.lib.phy_class_info(self.ctx, ctypes.byref(ll[0]), ctypes.byref(ii[0]), ctypes.byref(ii[1]),
-                                           ctypes.byref(ll[1]), ctypes.byref(ii[2]), ctypes.byref(ii[3])),
-                   "phy_class_info")
+                                           ctypes.byref(ll[1]), ctypes.byref(ll[2]), ctypes.byref(ii[2]),
+                                           ctypes.byref(ii[3])), "phy_class_info")
         return dict(classes=ll[0].value, levels=ii[0].value, root_classes=ii[1].value, stage=ll[1].value,
-                    tiles=ii[2].value, spans=ii[3].value)
+                    staged=ll[2].value, tiles=ii[2].value, spans=ii[3].value)
 
     def timing_start(self):
         _lib.check(self.lib.phy_timing_start(self.ctx), "phy_timing_start")
