@@ -56,6 +56,10 @@ def parse():
     ap.add_argument("--engine", choices=["auto", "pattern", "class"], default="auto",
                     help="pattern sweep, class sweep (site repeats) or the context's automatic choice")
     ap.add_argument("--json-out", default=None)
+    ap.add_argument("--shard-of", type=int, default=0,
+                    help="synthetic: evaluate only the first of this many pattern shards on one GPU, with no "
+                         "collective -- what each rank of an N-GPU run computes (a projection, not the "
+                         "headline)")
     ap.add_argument("--dry-run", action="store_true",
                     help="launcher check only: ranks join a gloo group on the CPU, all-reduce their rank "
                          "ids and exit (no GPU, no evaluation)")
@@ -300,11 +304,17 @@ def main():
         prob = synthetic_problem(args.sites)
         draws = args.draws or 1
         shard_world, shard_rank = world, rank
+        if args.shard_of > 1:
+            if world > 1:
+                raise SystemExit("bench.py: --shard-of is a one-GPU projection; run it without a launcher")
+            shard_world = args.shard_of
     S, P = prob["tipcodes"].shape
     C = prob["C"]
 
     sl = ShardedLikelihood(prob["tipcodes"], prob["weights"], prob["peel0"], prob["rooted"], prob["model"],
                            C, shard_rank, shard_world, device=local, max_draws=draws)
+    if args.shard_of > 1:
+        sl.world = 1  # the projection: one shard's evaluation, no collective
     eng = sl.engine
     if args.engine != "auto":
         eng.set_engine(args.engine)
@@ -470,6 +480,7 @@ def main():
                 "taxa": S, "patterns": P, "patterns_per_rank": P_local, "categories": C,
                 "branches": B, "draws_per_step": draws,
                 "parallelism": ("replicas%d" % world) if batched else ("patterns%d" % world),
+                "projection_shard_of": args.shard_of or None,
             },
             "roofline": {
                 "bound": "hbm", "achieved": achieved, "peak": PEAK_HBM_GBPS, "unit": "GB/s",

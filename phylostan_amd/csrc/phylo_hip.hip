@@ -1944,8 +1944,13 @@ int launch_class(phy_ctx* ctx, int n, const double* d_blens, const double* d_mod
   }
   HIP_TRY(hipGetLastError());
   if (ctx->timing) HIP_TRY(hipEventRecord(e1, st));
-  hipLaunchKernelGGL(cls_gsum_kernel, dim3(B, dcn), dim3(1024), 0, st, (const double*)e->d_gpart,
-                     (const int*)e->d_gbase, (const int*)e->d_gcount, grows, gstride, B, C, std::max(e->ngs, 1));
+  if (e->max_gcount > 64)
+    hipLaunchKernelGGL(cls_gsum_kernel, dim3(B, dcn), dim3(1024), 0, st, (const double*)e->d_gpart,
+                       (const int*)e->d_gbase, (const int*)e->d_gcount, grows, gstride, B, C, std::max(e->ngs, 1));
+  else
+    hipLaunchKernelGGL(cls_gsum_small_kernel, dim3((unsigned)(((long long)dcn * B * 16 + 255) / 256)), dim3(256), 0,
+                       st, (const double*)e->d_gpart, (const int*)e->d_gbase, (const int*)e->d_gcount, grows, gstride,
+                       B, C, std::max(e->ngs, 1), dcn);
   if (d_site)
     hipLaunchKernelGGL(cls_site_kernel, dim3((ctx->P + 255) / 256, n), dim3(256), 0, st,
                        (const double*)e->d_sitecls, (const int*)e->d_pat_root, d_site, ctx->P, e->nroot);

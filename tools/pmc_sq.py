@@ -31,14 +31,25 @@ def main():
         if r.returncode != 0:
             print("pass %d failed: %s" % (k, r.stderr.decode()[-2000:]), file=sys.stderr)
             continue
-        acc = {}
+        # pattern sweep: average per sweep_kernel dispatch; class sweep: the
+        # sum over one evaluation's cls_* dispatches (evaluations counted by
+        # cls_root_ll_kernel)
+        cls = "class" in bench_args
+        acc, nev = {}, {}
         for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
             for row in csv.DictReader(open(f)):
-                if "sweep_kernel" not in row["Kernel_Name"]:
+                name = row["Kernel_Name"]
+                if cls:
+                    if "cls_" not in name or "gsum" in name or "site" in name:
+                        continue
+                elif "sweep_kernel" not in name:
                     continue
-                acc.setdefault(row["Counter_Name"], []).append(float(row["Counter_Value"]))
+                cn = row["Counter_Name"]
+                acc[cn] = acc.get(cn, 0.0) + float(row["Counter_Value"])
+                if not cls or "cls_root_ll_kernel" in name:
+                    nev[cn] = nev.get(cn, 0) + 1
         for cn, v in acc.items():
-            out[cn] = sum(v) / len(v)
+            out[cn] = v / max(nev.get(cn, 1), 1)
     print(json.dumps(out, indent=1))
 
 
