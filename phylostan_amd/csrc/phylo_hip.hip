@@ -182,8 +182,10 @@ __device__ __forceinline__ double wave_sum(double v) {
 // Cross-lane moves on doubles (two 32-bit halves each).
 template <int CTRL>
 __device__ __forceinline__ double dpp_d(double v) {
-  const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(v), CTRL, 0xF, 0xF, false);
-  const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(v), CTRL, 0xF, 0xF, false);
+  // every lane has a valid source for the controls used here, so the old
+  // value is dead: mov_dpp leaves it undefined (no zeroing v_mov per half)
+  const int lo = __builtin_amdgcn_mov_dpp(__double2loint(v), CTRL, 0xF, 0xF, false);
+  const int hi = __builtin_amdgcn_mov_dpp(__double2hiint(v), CTRL, 0xF, 0xF, false);
   return __hiloint2double(hi, lo);
 }
 // v_permlane32_swap (gfx950): a <- [a_lo | b_lo], b <- [a_hi | b_hi]  (32-lane halves)
@@ -1248,14 +1250,14 @@ __global__ void __launch_bounds__(256) finalize_kernel(FinArgs a) {
   const size_t wg0 = (size_t)draw * a.gx;
   if (threadIdx.x < 16) Q[threadIdx.x] = a.eig[(size_t)draw * EIG_LEN + EIG_Q + threadIdx.x];
   {
-    // scalar partials per slot: [c][8] = ll (c = 0 only), dps_c, dfreq[4];
-    // quantity q is summed by wave q mod (waves), lanes striding over the
-    // slots, then a fixed-shape wave reduction (the same order whichever
-    // wave does it)
-    const int lane = threadIdx.x & (WAVE - 1);
+    // scalar partials per slot: [c][8] = ll (c = 0 only), dps_c, dfreq[4].
+    // One quantity at a time over the whole workgroup: thread t sums slots
+    // t, t + 256, ... (four in flight), then a fixed-order tree over the
+    // threads' partials in LDS (the class sweep has thousands of slots; with
+    // one slot -- one workgroup per draw -- the result is that slot exactly)
     const int nq = 2 + C + 4;  // ll, dps_0..C-1, dfreq_0..3 (+1 spare)
-    for (int q = threadIdx.x / WAVE; q < nq - 1; q += blockDim.x / WAVE) {
-      // four slots in flight per lane (four accumulators, fixed combine order)
+    double* red = fsh + (size_t)C * B + 16;  // blockDim.x doubles past inner[C*B] and Q[16]
+    for (int q = 0; q < nq - 1; ++q) {
       auto slot_val = [&](int w) -> double {
         const double* ss = a.sslot + (wg0 + w) * C * 8;
         if (q == 0) return ss[0];
@@ -1265,16 +1267,21 @@ __global__ void __launch_bounds__(256) finalize_kernel(FinArgs a) {
         return t;
       };
       double acc4[4] = {0.0, 0.0, 0.0, 0.0};
-      for (int w0 = lane; w0 < a.gx; w0 += 4 * WAVE) {
+      for (int w0 = threadIdx.x; w0 < a.gx; w0 += 4 * blockDim.x) {
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
-          const int w = w0 + u * WAVE;
+          const int w = w0 + u * blockDim.x;
           acc4[u] += (w < a.gx) ? slot_val(w) : 0.0;
         }
       }
-      double acc = (acc4[0] + acc4[1]) + (acc4[2] + acc4[3]);
-      acc = wave_sum(acc);
-      if (lane == 0) {
+      red[threadIdx.x] = (acc4[0] + acc4[1]) + (acc4[2] + acc4[3]);
+      __syncthreads();
+      for (int h = blockDim.x / 2; h > 0; h >>= 1) {
+        if ((int)threadIdx.x < h) red[threadIdx.x] += red[threadIdx.x + h];
+        __syncthreads();
+      }
+      if (threadIdx.x == 0) {
+        const double acc = red[0];
         if (q == 0)
           out[0] = isfinite(acc) ? acc : -INFINITY;
         else if (q <= C)
@@ -1282,6 +1289,7 @@ __global__ void __launch_bounds__(256) finalize_kernel(FinArgs a) {
         else
           out[1 + B + 2 * C + (q - 1 - C)] = acc;
       }
+      __syncthreads();
     }
   }
   __syncthreads();  // dL/dP rows and Q visible to the whole workgroup
@@ -1957,7 +1965,7 @@ int launch_class(phy_ctx* ctx, int n, const double* d_blens, const double* d_mod
   FinArgs fa{ctx->d_gslot, e->d_sslot, ctx->d_pmat, ctx->d_eig, d_blens, d_model, ctx->d_gpos, ctx->d_inner, d_out,
              C,            B,          ctx->nmat,   e->nrootch,  phy_output_len(ctx), 0, ctx->R, grows, gstride,
              ctx->kind};
-  hipLaunchKernelGGL(finalize_kernel, dim3(n), dim3(256), ((size_t)C * B + 16) * sizeof(double), st, fa);
+  hipLaunchKernelGGL(finalize_kernel, dim3(n), dim3(256), ((size_t)C * B + 16 + 256) * sizeof(double), st, fa);
   HIP_TRY(hipGetLastError());
   return PHY_OK;
 }
@@ -2034,7 +2042,7 @@ int launch_pattern(phy_ctx* ctx, int n, const double* d_blens, const double* d_m
     HIP_TRY(hipGetLastError());
   }
   if (!fin) {
-    hipLaunchKernelGGL(finalize_kernel, dim3(n), dim3(256), ((size_t)C * B + 16) * sizeof(double), st, fa);
+    hipLaunchKernelGGL(finalize_kernel, dim3(n), dim3(256), ((size_t)C * B + 16 + 256) * sizeof(double), st, fa);
     HIP_TRY(hipGetLastError());
   }
   return PHY_OK;
