@@ -284,7 +284,11 @@ struct SweepArgs {
 //          entries [0, ndl) kept in LDS), or K x 64 doubles when ndl = 0;
 //          wave c's root-exchange slice (K x 64 doubles) sits at the start
 //          of its own tail, whose deep entries are all free at the root
-__host__ __device__ inline size_t tip_lds_bytes(int S, int K) { return ((size_t)S * WAVE * K / 2 + 15) / 16 * 16; }
+// tips: the block's nibbles, then the 0/1 state vectors of the 16 record
+// indices (the t of dL/dP += r (x) t for a tip child: two LDS reads instead
+// of unpacking and converting its mask bits per column)
+__host__ __device__ inline size_t tip_nib_bytes(int S, int K) { return ((size_t)S * WAVE * K / 2 + 15) / 16 * 16; }
+__host__ __device__ inline size_t tip_lds_bytes(int S, int K) { return tip_nib_bytes(S, K) + 16 * 4 * sizeof(double); }
 __host__ __device__ inline size_t tail_doubles(int K, int ndl) {  // per wave
   return ndl > 0 ? (size_t)ndl * K * 2 * WAVE * 2 : (size_t)K * WAVE;
 }
@@ -304,14 +308,17 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* base, ui
   void* p = reinterpret_cast<void*>(((uint64_t)hi << 32) | lo);
   return __builtin_amdgcn_make_buffer_rsrc(p, (short)0, (int)n, 0x00020000);
 }
-// One stored 4-vector: two 16-B halves `half` bytes apart.  Every stored
+// One stored 4-vector: two 16-B halves `half` bytes apart (the wave-uniform
+// `half` rides in the instruction's soffset: no per-lane add; an
+// out-of-range `off` is out of range with or without it).  Every stored
 // partial is read exactly once, so the loads are non-temporal (aux 2 = nt):
 // measured +13% (fluA) / +3% (synthetic) over the default policy, with the
 // stores left at the default (nt or sc1 stores measured no better).
 constexpr int LOAD_NT = 2;
+constexpr uint32_t OOB = 0x40000000u;  // out-of-range offset part (regions are < 2^30 bytes, checked at plan time)
 __device__ __forceinline__ V4 ld_v4(__amdgpu_buffer_rsrc_t srd, uint32_t off, uint32_t half) {
   const auto lo = __builtin_amdgcn_raw_buffer_load_b128(srd, off, 0, LOAD_NT);
-  const auto hi = __builtin_amdgcn_raw_buffer_load_b128(srd, off + half, 0, LOAD_NT);
+  const auto hi = __builtin_amdgcn_raw_buffer_load_b128(srd, off, half, LOAD_NT);  // half in soffset
   V4 r;
   r.x = __hiloint2double((int)lo[1], (int)lo[0]);
   r.y = __hiloint2double((int)lo[3], (int)lo[2]);
@@ -329,7 +336,7 @@ __device__ __forceinline__ void st_v4(__amdgpu_buffer_rsrc_t srd, uint32_t off, 
   const u4 hi = {(unsigned)__double2loint(v.z), (unsigned)__double2hiint(v.z), (unsigned)__double2loint(v.w),
                  (unsigned)__double2hiint(v.w)};
   __builtin_amdgcn_raw_buffer_store_b128(lo, srd, off, 0, 0);
-  __builtin_amdgcn_raw_buffer_store_b128(hi, srd, off + half, 0, 0);
+  __builtin_amdgcn_raw_buffer_store_b128(hi, srd, off, half, 0);
 }
 
 // s_waitcnt vmcnt(0) that the compiler's waitcnt pass sees (an inline-asm
@@ -381,6 +388,12 @@ __device__ __forceinline__ V4 tipvec_b(unsigned b, unsigned long long extra) {
   const unsigned m = b < 4 ? (1u << b) : (unsigned)(extra >> (4 * (b - 4))) & 15u;
   return {(double)(m & 1u), (double)((m >> 1) & 1u), (double)((m >> 2) & 1u), (double)((m >> 3) & 1u)};
 }
+// The same, from the sweep's LDS table.
+__device__ __forceinline__ V4 tipvec_l(const double* tvec, unsigned b) {
+  const double2 lo = *reinterpret_cast<const double2*>(tvec + (b & 15u) * 4);
+  const double2 hi = *reinterpret_cast<const double2*>(tvec + (b & 15u) * 4 + 2);
+  return {lo.x, lo.y, hi.x, hi.y};
+}
 
 // The sweep.  `prog` is a separate __restrict__ const argument so the
 // backend proves it read-only and uses scalar loads.
@@ -419,6 +432,12 @@ __global__ void __launch_bounds__(MAXT) __attribute__((amdgpu_waves_per_eu(K == 
 
   unsigned char* tipl = lds_raw;
   double* mats0 = reinterpret_cast<double*>(lds_raw + tip_lds_bytes(a.S, K));
+  double* tvec = reinterpret_cast<double*>(lds_raw + tip_nib_bytes(a.S, K));  // [16][4]
+  if (threadIdx.x < 64) {  // published by the block loop's first barrier
+    const unsigned b = threadIdx.x >> 2, j = threadIdx.x & 3;
+    const unsigned m = b < 4 ? (1u << b) : (unsigned)(a.extra >> (4 * (b - 4))) & 15u;
+    tvec[threadIdx.x] = (double)((m >> j) & 1u);
+  }
   double* mats = mats0 + (size_t)c * a.cap_m * rec;
   const int ndl = DL ? a.ndeep : a.ndl;  // deep entries [0, ndl) live in LDS
   double* tail0 = mats0 + (size_t)C * a.cap_m * rec;
@@ -437,17 +456,25 @@ __global__ void __launch_bounds__(MAXT) __attribute__((amdgpu_waves_per_eu(K == 
   const __amdgpu_buffer_rsrc_t srd_dsk = make_rsrc(dsk, dsk_bytes);
   const int colw = c * WAVE + lane;  // this lane's column inside an entry half
   const uint32_t half_bytes = (uint32_t)ncolwg * 16u;
-  auto eoff = [&](int e, int k) __attribute__((always_inline)) -> uint32_t {  // byte offset of (entry, column k), half 0
-    return (uint32_t)((((size_t)e * K + k) * 2 * ncolwg + colw) * 16);
+  // Byte offset of (entry e, column k), half 0 = a per-lane column part plus
+  // the wave-uniform e * estr.  An operand that is not loaded gets the
+  // uniform part OOB instead (>= every region's size, so the sum is out of
+  // range and the load returns zeros): the choice is one scalar select, no
+  // per-lane select or exec masking.
+  const uint32_t estr = (uint32_t)(K * 2 * ncolwg * 16);
+  uint32_t lcol[K];  // this lane's column part
+#pragma unroll
+  for (int k = 0; k < K; ++k) lcol[k] = (uint32_t)((k * 2 * ncolwg + colw) * 16);
+  auto ent = [&](bool use, int e) __attribute__((always_inline)) -> uint32_t {  // uniform part
+    return use ? (uint32_t)e * estr : OOB;
   };
   // Scratch offsets of this lane's live columns only: padding columns
-  // (pattern >= P) neither store nor load moved partials -- the range check
-  // drops their stores and zero-fills their loads, so they stay finite and
-  // their weight-0 upper partials are exactly zero.
-  unsigned vbits = 0;  // bit k: column k of the current block is a pattern
-  auto soff = [&](int e, int k) __attribute__((always_inline)) -> uint32_t {
-    return ((vbits >> k) & 1u) ? eoff(e, k) : scr_bytes;
-  };
+  // (pattern >= P) get the column part OOB, so they neither store nor load
+  // moved partials -- the range check drops their stores and zero-fills
+  // their loads, so they stay finite and their weight-0 upper partials are
+  // exactly zero.
+  uint32_t lofs[K];  // per block: lcol[k], or OOB on a padding column
+  auto soff = [&](int e, int k) __attribute__((always_inline)) -> uint32_t { return lofs[k] + (uint32_t)e * estr; };
   auto put = [&](double2* base, int e, int k, const V4& v) __attribute__((always_inline)) {
     double2* d = base + ((size_t)e * K + k) * 2 * ncolwg + colw;
     d[0] = make_double2(v.x, v.y);
@@ -545,9 +572,8 @@ __global__ void __launch_bounds__(MAXT) __attribute__((amdgpu_waves_per_eu(K == 
   };
 
   for (int blk = blockIdx.x; blk < a.nblk; blk += gridDim.x) {
-    vbits = 0;
 #pragma unroll
-    for (int k = 0; k < K; ++k) vbits |= (blk * WAVE * K + k * WAVE + lane < a.P) ? (1u << k) : 0u;
+    for (int k = 0; k < K; ++k) lofs[k] = (blk * WAVE * K + k * WAVE + lane < a.P) ? lcol[k] : OOB;
     __syncthreads();  // the previous block's tip / root-exchange reads are done
     // stage this block's tip bytes in LDS: S rows x 64K bytes, shared by the
     // C category-waves and by both passes (8 loads in flight per thread)
@@ -592,7 +618,7 @@ __global__ void __launch_bounds__(MAXT) __attribute__((amdgpu_waves_per_eu(K == 
         const bool need = more && (sn.fl & F_XDEEP) && sn.xd >= ndl;                      \
         if (!DL)                                                                                                      \
       _Pragma("unroll")                                                                                               \
-        for (int k = 0; k < K; ++k) dnext[k] = ld_v4(srd_scr, need ? soff(sn.xs, k) : scr_bytes, half_bytes);         \
+        for (int k = 0; k < K; ++k) dnext[k] = ld_v4(srd_scr, lofs[k] + ent(need, sn.xs), half_bytes);         \
       }                                                                                                               \
       ensure_chunk(st);                                                                                               \
       const int x = st.x, y = st.y, fl = st.fl, vs = st.vs;                        \
@@ -721,10 +747,10 @@ __global__ void __launch_bounds__(MAXT) __attribute__((amdgpu_waves_per_eu(K == 
       const int xs = r.st.xs, ys = r.st.ys, vd = r.st.vd;                 \
       _Pragma("unroll")                                                          \
       for (int k = 0; k < K; ++k) {                                              \
-        r.lx[k] = ld_v4(srd_scr, lx ? soff(xs, k) : scr_bytes, half_bytes);      \
-        r.ly[k] = ld_v4(srd_scr, ly ? soff(ys, k) : scr_bytes, half_bytes);      \
+        r.lx[k] = ld_v4(srd_scr, lofs[k] + ent(lx, xs), half_bytes);             \
+        r.ly[k] = ld_v4(srd_scr, lofs[k] + ent(ly, ys), half_bytes);             \
         if constexpr (!DL)                                                       \
-          r.lr[k] = ld_v4(srd_dsk, lr ? eoff(vd, k) : dsk_bytes, half_bytes);    \
+          r.lr[k] = ld_v4(srd_dsk, lcol[k] + ent(lr, vd), half_bytes);            \
       }                                                                          \
     } while (0)
     #define REBUILD(cst, out) do { /* a_c of a cherry c from LDS, as its forward step formed it */  \
@@ -827,13 +853,13 @@ __global__ void __launch_bounds__(MAXT) __attribute__((amdgpu_waves_per_eu(K == 
       if (XT) {                                                                   \
         V4 tv[K];                                                                 \
       _Pragma("unroll")                                                           \
-        for (int k = 0; k < K; ++k) tv[k] = tipvec_b(bx[k], a.extra);             \
+        for (int k = 0; k < K; ++k) tv[k] = tipvec_l(tvec, bx[k]);                \
         gacc(st.mx, rx, tv);                                                      \
       }                                                                           \
       if (YT) {                                                                   \
         V4 tv[K];                                                                 \
       _Pragma("unroll")                                                           \
-        for (int k = 0; k < K; ++k) tv[k] = tipvec_b(by[k], a.extra);             \
+        for (int k = 0; k < K; ++k) tv[k] = tipvec_l(tvec, by[k]);                \
         gacc(st.my, ry, tv);                                                      \
       }                                                                           \
       if (!XT && !YT) { /* r_x waits on the deep stack while y's subtree runs */  \
@@ -1753,6 +1779,8 @@ int waves_per_simd(int K) { return K == 2 ? PHY_WPE2 : 4; }  // the kernel's reg
 int plan_chunks(phy_ctx* c) {
   const int K = c->cols_pref ? c->cols_pref : (c->C <= 8 ? 2 : 1);
   if (K == 2 && c->C > 8) return fail(PHY_EINVAL, "two columns per lane need C <= 8");
+  if ((size_t)std::max(c->nslots, c->ndeep) * K * 2 * c->C * WAVE * 16 >= (size_t)OOB)
+    return fail(PHY_EINVAL, "per-workgroup scratch region too large for 32-bit buffer offsets");
   int ndl = 0;  // deep-stack entries held in LDS
   auto cap_for = [&](size_t budget) {
     int cap = c->nmat;
