@@ -55,7 +55,8 @@ constexpr int WAVE = 64;
 #ifndef PHY_ABLATE
 // Diagnostic builds only (timing of the sweep's pieces; results are wrong by
 // construction): 2 = no reverse pass, 4 = no per-draw epilogue, 8 = no
-// moved-partial stores.
+// moved-partial stores, 16 = every store to entry 0 (L2-resident), 32 =
+// every operand load from entry 0.
 #define PHY_ABLATE 0
 #endif
 // Program step (STEP_INTS ints, host-built by build_program).
@@ -466,7 +467,7 @@ __global__ void __launch_bounds__(MAXT) __attribute__((amdgpu_waves_per_eu(K == 
 #pragma unroll
   for (int k = 0; k < K; ++k) lcol[k] = (uint32_t)((k * 2 * ncolwg + colw) * 16);
   auto ent = [&](bool use, int e) __attribute__((always_inline)) -> uint32_t {  // uniform part
-    return use ? (uint32_t)e * estr : OOB;
+    return use ? ((PHY_ABLATE & 32) ? 0u : (uint32_t)e * estr) : OOB;
   };
   // Scratch offsets of this lane's live columns only: padding columns
   // (pattern >= P) get the column part OOB, so they neither store nor load
@@ -474,7 +475,9 @@ __global__ void __launch_bounds__(MAXT) __attribute__((amdgpu_waves_per_eu(K == 
   // their loads, so they stay finite and their weight-0 upper partials are
   // exactly zero.
   uint32_t lofs[K];  // per block: lcol[k], or OOB on a padding column
-  auto soff = [&](int e, int k) __attribute__((always_inline)) -> uint32_t { return lofs[k] + (uint32_t)e * estr; };
+  auto soff = [&](int e, int k) __attribute__((always_inline)) -> uint32_t {
+    return lofs[k] + ((PHY_ABLATE & 16) ? 0u : (uint32_t)e * estr);
+  };
   auto put = [&](double2* base, int e, int k, const V4& v) __attribute__((always_inline)) {
     double2* d = base + ((size_t)e * K + k) * 2 * ncolwg + colw;
     d[0] = make_double2(v.x, v.y);

@@ -1,0 +1,120 @@
+"""ctypes binding of ``libphylo_host.so`` (csrc/host_model.cpp): native host
+pieces of the clock models -- heights transform, log-Jacobian, branch spans
+and the constant coalescent, with their reverse passes.
+
+The numpy restatements in ``posterior.py`` / ``priors.py`` stay the
+specification (``tests/test_hostlib.py`` compares the two); the posterior
+uses this library when it is built, because these loops are the per-round
+host cost of NUTS on a clock model.
+"""
+import ctypes
+import os
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("PHYLO_HOST_LIB") or os.path.join(_HERE, "libphylo_host.so")
+_lib = None
+
+# every pointer is passed as an address (c_void_p): cheaper per call than
+# typed ctypes pointers, which matters at one call per gradient round
+_D = _I = _U8 = ctypes.c_void_p
+_i = ctypes.c_int
+
+
+def load():
+    """The library, or None when it is not built."""
+    global _lib
+    if _lib is None and os.path.exists(LIB_PATH):
+        lib = ctypes.CDLL(LIB_PATH)
+        lib.phh_heights.argtypes = [_i, _i, _i, _I, _I, _I, _D, _i, _i, _D, _D, _D]
+        lib.phh_heights_back.argtypes = [_i, _i, _i, _I, _I, _I, _D, _i, _i, _D, _D, _D, _D, _D]
+        lib.phh_height_jacobian.argtypes = [_i, _i, _i, _I, _D, _D, _D, _D]
+        lib.phh_span.argtypes = [_i, _i, _i, _I, _I, _D, _D, _D]
+        lib.phh_span_back.argtypes = [_i, _i, _i, _I, _I, _D, _D]
+        lib.phh_constant_coalescent.argtypes = [_i, _i, _D, _U8, _D, _D, _D, _D]
+        for f in ("phh_heights", "phh_heights_back", "phh_height_jacobian", "phh_span", "phh_span_back",
+                  "phh_constant_coalescent"):
+            getattr(lib, f).restype = None
+        _lib = lib
+    return _lib
+
+
+def _d(a):
+    return a.ctypes.data
+
+
+def _c(a, dtype=np.float64):
+    return np.ascontiguousarray(a, dtype=dtype)
+
+
+class ClockTreeNative:
+    """Index arrays of one tree in the layout the native routines take."""
+
+    def __init__(self, S, order_nodes, order_par, order_prop, order_low, root_h, b_parent, b_hidx, b_internal,
+                 b_lower, jac_par, jac_low):
+        self.lib = load()
+        self.S = S
+        self.H = S - 1
+        self.np = S - 2
+        self.node = _c(order_nodes, np.int32)
+        self.par = _c(order_par, np.int32)
+        self.prop = _c(order_prop, np.int32)
+        self.low = _c(order_low)
+        self.m = len(self.node)
+        self.root = int(root_h)
+        self.bpar = _c(b_parent, np.int32)
+        self.bh = _c(np.where(b_internal, b_hidx, -1), np.int32)
+        self.blow = _c(b_lower)
+        self.B = len(self.bpar)
+        self.jpar = _c(jac_par, np.int32)
+        self.jlow = _c(jac_low)
+        # addresses of the static index arrays, resolved once
+        self.p_node, self.p_par, self.p_prop, self.p_low = (a.ctypes.data for a in (self.node, self.par, self.prop,
+                                                                                      self.low))
+        self.p_bpar, self.p_bh, self.p_blow = (a.ctypes.data for a in (self.bpar, self.bh, self.blow))
+        self.p_jpar, self.p_jlow = self.jpar.ctypes.data, self.jlow.ctypes.data
+
+    def heights(self, props, height):
+        props, height = _c(props), _c(height)
+        n = props.shape[0]
+        h = np.empty((n, self.H))
+        self.lib.phh_heights(n, self.H, self.m, self.p_node, self.p_par, self.p_prop, self.p_low, self.root, self.np,
+                             _d(props), _d(height), _d(h))
+        return h
+
+    def heights_back(self, props, h, gh, gprops, gheight):
+        """In place: consumes gh, accumulates gprops [n, S-2] and gheight [n]."""
+        props, h = _c(props), _c(h)
+        n = props.shape[0]
+        self.lib.phh_heights_back(n, self.H, self.m, self.p_node, self.p_par, self.p_prop, self.p_low, self.root,
+                                  self.np, _d(props), _d(h), _d(gh), _d(gprops), _d(gheight))
+
+    def jacobian(self, h, lp, gh):
+        h = _c(h)
+        self.lib.phh_height_jacobian(h.shape[0], self.H, len(self.jpar), self.p_jpar, self.p_jlow, _d(h), _d(lp),
+                                     _d(gh))
+
+    def span(self, h):
+        h = _c(h)
+        out = np.empty((h.shape[0], self.B))
+        self.lib.phh_span(h.shape[0], self.H, self.B, self.p_bpar, self.p_bh, self.p_blow, _d(h), _d(out))
+        return out
+
+    def span_back(self, gspan, gh):
+        gspan = _c(gspan)
+        self.lib.phh_span_back(gspan.shape[0], self.H, self.B, self.p_bpar, self.p_bh, _d(gspan), _d(gh))
+
+
+def constant_coalescent(times, internal, theta):
+    """Native ``priors.constant_coalescent``: (logP [n], dtimes [n, N], dtheta [n])."""
+    lib = load()
+    times = _c(times)
+    n, N = times.shape
+    intl = _c(internal, np.uint8)
+    theta = _c(theta)
+    lp = np.empty(n)
+    g = np.empty((n, N))
+    dth = np.empty(n)
+    lib.phh_constant_coalescent(n, N, _d(times), intl.ctypes.data, _d(theta), _d(lp), _d(g), _d(dth))
+    return lp, g, dth

@@ -27,10 +27,12 @@ strict`` with ``--estimate_rate`` or a fixed ``--rate``, or a relaxed clock
 Phylogeography (``--geo``) is refused loudly.
 """
 import math
+import os
 
 import numpy as np
 
 from . import clocks
+from . import hostlib
 from . import models
 from . import priors
 from . import transforms
@@ -155,6 +157,8 @@ class Posterior:
             off += p.tr.size
         self.dim = off
         self.const = self._dropped_constants()
+        i = np.arange(1, self.C + 1, dtype=np.float64)
+        self._wx = -np.log(1.0 - (2.0 * (i - 1) + 1.0) / (2.0 * self.C))  # Weibull quantile bases
 
     # ------------------------------------------------------------------ layout
     def _declare(self):
@@ -274,6 +278,14 @@ class Posterior:
         self.times_internal = np.zeros(2 * S - 1, bool)
         self.times_internal[S:] = True
         self.ctree = clocks.ClockTree(S, t.map1) if self.spec.relaxed else None
+        # native routines for the same loops (hostlib), when built
+        self._nat = None
+        if hostlib.load() is not None and os.environ.get("PHYLO_HOST_NATIVE", "1") != "0":
+            cat = (lambda k: np.concatenate([lv[k] for lv in self.levels])) if self.levels else \
+                (lambda k: np.zeros(0))
+            self._nat = hostlib.ClockTreeNative(
+                S, cat(0) - S, cat(1), cat(2), cat(3), self.root - S, self.b_parent, self.b_hidx, self.b_internal,
+                self.b_lower, parent[nonroot_int] - S, self.lowers[nonroot_int])
 
     def _dropped_constants(self):
         """Normalising constants Stan's ``~`` statements drop (propto) -- added
@@ -324,10 +336,9 @@ class Posterior:
                 for d in range(n):
                     rs[d], ps[d] = models.weibull_pinv_site_rates(w[d], pinv[d], C)
                 return rs, ps
-            rs = np.empty((n, C))
-            for d in range(n):
-                rs[d] = models.weibull_site_rates(w[d], C)[0]
-            return rs, np.full((n, C), 1.0 / C)
+            # models.weibull_site_rates, all draws at once
+            g = np.power(self._wx[None, :], 1.0 / w[:, None])
+            return g / (g.sum(axis=1, keepdims=True) / C), np.full((n, C), 1.0 / C)
         if sp.categories > 1:
             ps = vals["ps"]
             ru = vals["rate_unscaled"]
@@ -341,6 +352,8 @@ class Posterior:
         return np.ones((n, 1)), np.ones((n, 1))
 
     def _heights(self, vals, n):
+        if self._nat is not None:
+            return self._nat.heights(vals["props"], vals["height"])
         S = self.S
         h = np.empty((n, S - 1))
         h[:, self.root - S] = vals["height"]
@@ -351,6 +364,8 @@ class Posterior:
 
     def _span(self, h):
         """Branch durations [n, B]: heights[parent] - heights[node] (tips: - lowers)."""
+        if self._nat is not None:
+            return self._nat.span(h)
         base = np.where(self.b_internal, h[:, self.b_hidx], self.b_lower)
         return h[:, self.b_parent] - base
 
@@ -422,21 +437,35 @@ class Posterior:
         inside their declared bounds (a draw outside is a Stan domain
         error: rejected with lp = -inf before anything is evaluated)."""
         U = np.atleast_2d(np.asarray(U, np.float64))
-        n = U.shape[0]
-        ok = np.all(np.isfinite(U), axis=1)
         with np.errstate(all="ignore"):
-            vals, _, logj = self.constrain(np.where(np.isfinite(U), U, 0.0))
-            ok &= np.isfinite(logj)
-            for p in self.params:
-                x = np.asarray(vals[p.name], np.float64).reshape(n, -1)
-                ok &= np.all(np.isfinite(x), axis=1)
-                if isinstance(p.tr, transforms.Lower):
-                    ok &= np.all(x > p.tr.lower, axis=1)
-                elif isinstance(p.tr, transforms.Unit):
-                    ok &= np.all((x > 0.0) & (x < 1.0), axis=1)
-                elif isinstance(p.tr, transforms.Simplex):
-                    ok &= np.all(x > 0.0, axis=1)
-        return ok
+            return self._support(U, *self.constrain(np.where(np.isfinite(U), U, 0.0)))[0]
+
+    def _bounds(self):
+        """Strict open bounds (lo, hi) of every constrained coordinate."""
+        lo, hi = [], []
+        for p in self.params:
+            k = int(np.prod(p.tr.shape)) if p.tr.shape else 1
+            if isinstance(p.tr, transforms.Lower):
+                a, b = p.tr.lower, np.inf
+            elif isinstance(p.tr, transforms.Unit):
+                a, b = 0.0, 1.0
+            elif isinstance(p.tr, transforms.Simplex):
+                a, b = 0.0, np.inf
+            else:
+                a, b = -np.inf, np.inf
+            lo += [a] * k
+            hi += [b] * k
+        return np.array(lo), np.array(hi)
+
+    def _support(self, U, vals, states, logj):
+        """in_support on already-constrained values (one vector test)."""
+        n = U.shape[0]
+        if not hasattr(self, "_lo"):
+            self._lo, self._hi = self._bounds()
+        X = np.concatenate([np.asarray(vals[p.name], np.float64).reshape(n, -1) for p in self.params], axis=1)
+        ok = (np.isfinite(U).all(axis=1) & np.isfinite(logj)
+              & (np.isfinite(X) & (X > self._lo) & (X < self._hi)).all(axis=1))
+        return ok, vals, states, logj
 
     def log_prob_grad(self, U, propto=True, need_grad=True):
         """(lp [n], grad [n, dim]) at unconstrained draws U [n, dim]
@@ -448,22 +477,27 @@ class Posterior:
         rejected the same way after evaluation."""
         U = np.atleast_2d(np.asarray(U, np.float64))
         n = U.shape[0]
-        ok = self.in_support(U)
+        with np.errstate(all="ignore"):
+            ok, vals, states, logj = self._support(U, *self.constrain(np.where(np.isfinite(U), U, 0.0)))
         lp = np.full(n, -np.inf)
         G = np.zeros((n, self.dim)) if need_grad else None
         if ok.any():
+            pre = None
+            if ok.all():  # the usual case: the constrained values are reused
+                pre = (vals, states, logj)
             with np.errstate(all="ignore"):
-                lp_ok, g_ok = self._log_prob_grad_rows(U[ok], propto, need_grad)
+                lp_ok, g_ok = self._log_prob_grad_rows(U[ok], propto, need_grad, pre)
             lp[ok] = lp_ok
             if need_grad:
                 G[ok] = g_ok
         return lp, G
 
-    def _log_prob_grad_rows(self, U, propto=True, need_grad=True):
+    def _log_prob_grad_rows(self, U, propto=True, need_grad=True, pre=None):
         n = U.shape[0]
         sp = self.spec
         S, C = self.S, self.C
-        vals, states, lp = self.constrain(U)
+        vals, states, lp = self.constrain(U) if pre is None else pre
+        lp = np.array(lp, np.float64)
         gx = {p.name: np.zeros((n,) + p.tr.shape) for p in self.params}
 
         # ---- substitution / site models
@@ -524,10 +558,15 @@ class Posterior:
                 gx["netDiversificationRate"] += g_a
                 gx["relativeExtinctionRate"] += g_r
             # log-Jacobian of the height transform (generate_script.py:739-752)
-            nr = self.nonroot_int
-            gap = h[:, self.parent[nr] - S] - self.lowers[nr]
-            lp = lp + np.log(gap).sum(axis=1)
-            np.add.at(g_h.T, self.parent[nr] - S, (1.0 / gap).T)
+            if self._nat is not None:
+                jl = np.zeros(n)
+                self._nat.jacobian(h, jl, g_h)
+                lp = lp + jl
+            else:
+                nr = self.nonroot_int
+                gap = h[:, self.parent[nr] - S] - self.lowers[nr]
+                lp = lp + np.log(gap).sum(axis=1)
+                np.add.at(g_h.T, self.parent[nr] - S, (1.0 / gap).T)
             # coalescent
             if sp.coalescent is not None:
                 times = np.empty((n, 2 * S - 1))
@@ -535,7 +574,8 @@ class Posterior:
                 times[:, S:] = h
                 if sp.coalescent == "constant":
                     th = vals["theta"]
-                    c_lp, g_t, g_th = priors.constant_coalescent(times, self.times_internal, th)
+                    coal = hostlib.constant_coalescent if self._nat is not None else priors.constant_coalescent
+                    c_lp, g_t, g_th = coal(times, self.times_internal, th)
                     lp = lp + c_lp - np.log(th)  # theta ~ oneOnX()
                     gx["theta"] += g_th - 1.0 / th
                 else:
@@ -591,17 +631,21 @@ class Posterior:
                     gx["substrates"] += g_subs
             elif sp.estimate_rate:
                 gx["rate"] += g_mult.sum(axis=1)
-            np.add.at(g_h.T, self.b_parent, gspan.T)
-            np.add.at(g_h.T, self.b_hidx[self.b_internal], -gspan[:, self.b_internal].T)
-            # heights <- props, height (reverse of the level sweep)
-            props = vals["props"]
-            gprops = np.zeros_like(props)
-            for nodes, pidx, jidx, low in reversed(self.levels):
-                gn = g_h[:, nodes - S]
-                gprops[:, jidx] += gn * (h[:, pidx] - low)
-                np.add.at(g_h.T, pidx, (gn * props[:, jidx]).T)
-            gx["props"] += gprops
-            gx["height"] += g_h[:, self.root - S]
+            if self._nat is not None:
+                self._nat.span_back(gspan, g_h)
+                self._nat.heights_back(vals["props"], h, g_h, gx["props"], gx["height"])
+            else:
+                np.add.at(g_h.T, self.b_parent, gspan.T)
+                np.add.at(g_h.T, self.b_hidx[self.b_internal], -gspan[:, self.b_internal].T)
+                # heights <- props, height (reverse of the level sweep)
+                props = vals["props"]
+                gprops = np.zeros_like(props)
+                for nodes, pidx, jidx, low in reversed(self.levels):
+                    gn = g_h[:, nodes - S]
+                    gprops[:, jidx] += gn * (h[:, pidx] - low)
+                    np.add.at(g_h.T, pidx, (gn * props[:, jidx]).T)
+                gx["props"] += gprops
+                gx["height"] += g_h[:, self.root - S]
         else:
             gx["blens"] += g_bl
 
@@ -635,8 +679,13 @@ class Posterior:
                     gx["wshape"][d] += (g_rs[d, 1:] * drs_w).sum()
                     gx["pinv"][d] += (g_rs[d, 1:] * drs_p).sum() + g_ps[d, 0] - g_ps[d, 1:].sum() / cat
                 return
-            for d in range(len(w)):
-                gx["wshape"][d] += (g_rs[d] * models.weibull_site_rates_dshape(w[d], C)).sum()
+            # models.weibull_site_rates_dshape, all draws at once
+            x = self._wx[None, :]
+            g = np.power(x, 1.0 / w[:, None])
+            dg = g * np.log(x) * (-1.0 / (w * w))[:, None]
+            m = g.mean(axis=1, keepdims=True)
+            dm = dg.mean(axis=1, keepdims=True)
+            gx["wshape"] += (g_rs * (dg / m - g * dm / (m * m))).sum(axis=1)
             return
         if sp.categories > 1:
             p_ = vals["ps"]
