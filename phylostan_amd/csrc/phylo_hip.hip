@@ -1280,45 +1280,47 @@ __global__ void __launch_bounds__(256) finalize_kernel(FinArgs a) {
   if (threadIdx.x < 16) Q[threadIdx.x] = a.eig[(size_t)draw * EIG_LEN + EIG_Q + threadIdx.x];
   {
     // scalar partials per slot: [c][8] = ll (c = 0 only), dps_c, dfreq[4].
-    // One quantity at a time over the whole workgroup: thread t sums slots
-    // t, t + 256, ... (four in flight), then a fixed-order tree over the
-    // threads' partials in LDS (the class sweep has thousands of slots; with
-    // one slot -- one workgroup per draw -- the result is that slot exactly)
-    const int nq = 2 + C + 4;  // ll, dps_0..C-1, dfreq_0..3 (+1 spare)
+    // Thread t owns element k = t % (8C) of the slot records and sums it over
+    // the slots of its group g = t / (8C) (slots g, g + G, ...: one
+    // coalesced 8C-double record per group per step, four in flight), then
+    // thread k sums the G group partials in group order -- a fixed order,
+    // and with a single slot (one workgroup per draw) exactly that slot.
+    const int E = 8 * C;
+    const int G = max(1, (int)blockDim.x / E);
     double* red = fsh + (size_t)C * B + 16;  // blockDim.x doubles past inner[C*B] and Q[16]
-    for (int q = 0; q < nq - 1; ++q) {
-      auto slot_val = [&](int w) -> double {
-        const double* ss = a.sslot + (wg0 + w) * C * 8;
-        if (q == 0) return ss[0];
-        if (q <= C) return ss[(q - 1) * 8 + 1];
-        double t = 0.0;
-        for (int c = 0; c < C; ++c) t += ss[c * 8 + 2 + (q - 1 - C)];
-        return t;
-      };
-      double acc4[4] = {0.0, 0.0, 0.0, 0.0};
-      for (int w0 = threadIdx.x; w0 < a.gx; w0 += 4 * blockDim.x) {
+    const int g = threadIdx.x / E, k = threadIdx.x - g * E;
+    double acc = 0.0;
+    if (g < G && E <= (int)blockDim.x) {
+      const double* ss = a.sslot + wg0 * E + k;
+      for (int w0 = g; w0 < a.gx; w0 += 4 * G) {
+        double v[4];
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
-          const int w = w0 + u * blockDim.x;
-          acc4[u] += (w < a.gx) ? slot_val(w) : 0.0;
+          const int w = w0 + u * G;
+          v[u] = (w < a.gx) ? ss[(size_t)w * E] : 0.0;
         }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) acc += v[u];
       }
-      red[threadIdx.x] = (acc4[0] + acc4[1]) + (acc4[2] + acc4[3]);
-      __syncthreads();
-      for (int h = blockDim.x / 2; h > 0; h >>= 1) {
-        if ((int)threadIdx.x < h) red[threadIdx.x] += red[threadIdx.x + h];
-        __syncthreads();
+    }
+    red[threadIdx.x] = acc;
+    __syncthreads();
+    double tot = 0.0;
+    if ((int)threadIdx.x < E) {
+      for (int gg = 0; gg < G; ++gg) tot += red[gg * E + threadIdx.x];
+    }
+    __syncthreads();
+    if ((int)threadIdx.x < E) red[threadIdx.x] = tot;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      const double ll = red[0];
+      out[0] = isfinite(ll) ? ll : -INFINITY;
+      for (int c = 0; c < C; ++c) out[1 + B + C + c] = red[c * 8 + 1];
+      for (int f = 0; f < 4; ++f) {
+        double t = 0.0;
+        for (int c = 0; c < C; ++c) t += red[c * 8 + 2 + f];
+        out[1 + B + 2 * C + f] = t;
       }
-      if (threadIdx.x == 0) {
-        const double acc = red[0];
-        if (q == 0)
-          out[0] = isfinite(acc) ? acc : -INFINITY;
-        else if (q <= C)
-          out[1 + B + C + (q - 1)] = acc;
-        else
-          out[1 + B + 2 * C + (q - 1 - C)] = acc;
-      }
-      __syncthreads();
     }
   }
   __syncthreads();  // dL/dP rows and Q visible to the whole workgroup

@@ -17,4 +17,5 @@ timeout -k 10 300 python bench.py --workload HCV --json-out $O/HCV.json > $O/HCV
 timeout -k 10 300 python bench.py --workload DS1 --json-out $O/DS1.json > $O/DS1.log 2>&1 && \
 for n in 2 4 8; do timeout -k 10 300 python bench.py --workload synthetic --shard-of $n --steps 50 --warmup 5 --no-cpu-baseline --json-out $O/syn_shard$n.json > $O/syn_shard$n.log 2>&1 || exit $?; done && \
 timeout -k 10 400 python tools/pmc_sq.py --workload synthetic --engine class --steps 3 --warmup 1 --no-cpu-baseline > $O/sq_syn_class.json 2> $O/sq_syn_class.err && \
+timeout -k 10 400 python tools/pmc_sq.py --workload fluA --engine pattern --steps 3 --warmup 1 --no-cpu-baseline > $O/sq_fluA.json 2> $O/sq_fluA.err && \
 cat $O/fluA.json $O/syn.json && echo ALLDONE
