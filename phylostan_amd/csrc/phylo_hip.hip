@@ -1282,7 +1282,7 @@ __global__ void __launch_bounds__(256) finalize_kernel(FinArgs a) {
     // scalar partials per slot: [c][8] = ll (c = 0 only), dps_c, dfreq[4].
     // Thread t owns element k = t % (8C) of the slot records and sums it over
     // the slots of its group g = t / (8C) (slots g, g + G, ...: one
-    // coalesced 8C-double record per group per step, four in flight), then
+    // coalesced 8C-double record per group per step, 16 in flight), then
     // thread k sums the G group partials in group order -- a fixed order,
     // and with a single slot (one workgroup per draw) exactly that slot.
     const int E = 8 * C;
@@ -1292,15 +1292,16 @@ __global__ void __launch_bounds__(256) finalize_kernel(FinArgs a) {
     double acc = 0.0;
     if (g < G && E <= (int)blockDim.x) {
       const double* ss = a.sslot + wg0 * E + k;
-      for (int w0 = g; w0 < a.gx; w0 += 4 * G) {
-        double v[4];
+      constexpr int U = 16;  // loads in flight: thousands of slots are a latency chain otherwise
+      for (int w0 = g; w0 < a.gx; w0 += U * G) {
+        double v[U];
 #pragma unroll
-        for (int u = 0; u < 4; ++u) {
+        for (int u = 0; u < U; ++u) {
           const int w = w0 + u * G;
           v[u] = (w < a.gx) ? ss[(size_t)w * E] : 0.0;
         }
 #pragma unroll
-        for (int u = 0; u < 4; ++u) acc += v[u];
+        for (int u = 0; u < U; ++u) acc += v[u];
       }
     }
     red[threadIdx.x] = acc;
