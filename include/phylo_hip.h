@@ -198,6 +198,14 @@ int phy_engine(const phy_ctx* ctx);
 int phy_class_info(const phy_ctx* ctx, long long* classes, int* levels, int* root_classes, long long* stage,
                    long long* staged, int* tiles, int* spans);
 
+/* Bottom clades of the class plan: the levels 1..fused_levels run as one
+ * workgroup per clade (a maximal subtree of nodes at those levels) instead
+ * of one launch per level and phase; clades, and the classes of the largest.
+ * Chosen automatically (the deepest level whose largest clade has at most
+ * 1024 classes); PHY_CLADE=k at phy_create fixes k levels (0: off).
+ * Results are bitwise the same either way. */
+int phy_class_clades(const phy_ctx* ctx, int* fused_levels, int* clades, long long* largest);
+
 #ifdef __cplusplus
 }
 #endif

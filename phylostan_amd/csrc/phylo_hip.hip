@@ -1957,7 +1957,10 @@ int launch_class(phy_ctx* ctx, int n, const double* d_blens, const double* d_mod
   const int dcn = n * C;
   hipEvent_t e0 = nullptr, e1 = nullptr;
   if (ctx->timing && (rc = timing_begin(ctx, st, &e0, &e1))) return rc;
-  for (int l = 1; l < e->levels; ++l) {
+  if (e->Lc > 0)  // levels 1..Lc: one workgroup per (bottom clade, dc)
+    hipLaunchKernelGGL(cls_clade_fwd_kernel, dim3(e->nclade, dcn), dim3(CLADE_THREADS), 0, st, a,
+                       (const CladeLevel*)e->d_clade, e->Lc);
+  for (int l = e->Lc + 1; l < e->levels; ++l) {
     const ClassLevel& L = e->lv[l];
     if (!L.nchunk) continue;
     a.first = L.chunk0;
@@ -1966,7 +1969,7 @@ int launch_class(phy_ctx* ctx, int n, const double* d_blens, const double* d_mod
   }
   hipLaunchKernelGGL(cls_root_ll_kernel, dim3((e->nroot + 255) / 256, n), dim3(256), 0, st, a);
   hipLaunchKernelGGL(cls_root_rev_kernel, dim3(e->nrootch, dcn), dim3(64), 0, st, a);
-  for (int l = e->levels - 1; l >= 1; --l) {
+  for (int l = e->levels - 1; l > e->Lc; --l) {
     const ClassLevel& L = e->lv[l];
     if (L.ntile) {
       a.first = L.tile0;
@@ -1983,6 +1986,16 @@ int launch_class(phy_ctx* ctx, int n, const double* d_blens, const double* d_mod
       a.count = L.nchunk;
       hipLaunchKernelGGL(cls_rev_kernel, dim3((L.nchunk + 3) / 4, dcn), dim3(256), 0, st, a);
     }
+  }
+  if (e->Lc > 0) {
+    if (e->nrtile)
+      hipLaunchKernelGGL(cls_red_list_kernel, dim3((e->nrtile + 3) / 4, dcn), dim3(256), 0, st, a,
+                         (const int*)e->d_rtile, e->nrtile);
+    if (e->nrspan)
+      hipLaunchKernelGGL(cls_fix_list_kernel, dim3((e->nrspan + 3) / 4, dcn), dim3(256), 0, st, a,
+                         (const int*)e->d_rspan, e->nrspan);
+    hipLaunchKernelGGL(cls_clade_rev_kernel, dim3(e->nclade, dcn), dim3(CLADE_THREADS), 0, st, a,
+                       (const CladeLevel*)e->d_clade, e->Lc);
   }
   HIP_TRY(hipGetLastError());
   if (ctx->timing) HIP_TRY(hipEventRecord(e1, st));
@@ -2444,6 +2457,15 @@ int phy_class_info(const phy_ctx* ctx, long long* classes, int* levels, int* roo
   if (staged) *staged = e ? e->stage_sec : 0;
   if (tiles) *tiles = e ? e->ntiles : 0;
   if (spans) *spans = nspan;
+  return PHY_OK;
+}
+
+int phy_class_clades(const phy_ctx* ctx, int* fused_levels, int* clades, long long* largest) {
+  if (!ctx) return fail(PHY_EINVAL, "NULL ctx");
+  const ClassEngine* e = ctx->ce;
+  if (fused_levels) *fused_levels = e ? e->Lc : 0;
+  if (clades) *clades = e ? e->nclade : 0;
+  if (largest) *largest = e ? e->clade_max : 0;
   return PHY_OK;
 }
 

@@ -203,8 +203,12 @@ class TreeLikelihood:
         _lib.check(self.lib.phy_class_info(self.ctx, ctypes.byref(ll[0]), ctypes.byref(ii[0]), ctypes.byref(ii[1]),
                                            ctypes.byref(ll[1]), ctypes.byref(ll[2]), ctypes.byref(ii[2]),
                                            ctypes.byref(ii[3])), "phy_class_info")
+        fl, nc, big = ctypes.c_int(), ctypes.c_int(), ctypes.c_longlong()
+        _lib.check(self.lib.phy_class_clades(self.ctx, ctypes.byref(fl), ctypes.byref(nc), ctypes.byref(big)),
+                   "phy_class_clades")
         return dict(classes=ll[0].value, levels=ii[0].value, root_classes=ii[1].value, stage=ll[1].value,
-                    staged=ll[2].value, tiles=ii[2].value, spans=ii[3].value)
+                    staged=ll[2].value, tiles=ii[2].value, spans=ii[3].value, clade_levels=fl.value,
+                    clades=nc.value, clade_max=big.value)
 
     def timing_start(self):
         _lib.check(self.lib.phy_timing_start(self.ctx), "phy_timing_start")

@@ -128,3 +128,63 @@ def test_class_sweep_synthetic_200k_vs_c_port():
     _close(res.grad_rs, ref.grad_rs, RTOL_G, "grad_rs")
     _close(res.grad_ps, ref.grad_ps, RTOL_G, "grad_ps")
     _close(res.grad_freq_root, ref.grad_freq_root, RTOL_G, "grad_freq_root")
+
+
+def _with_clade(case, value, max_draws=1):
+    import os
+    old = os.environ.get("PHY_CLADE")
+    if value is None:
+        os.environ.pop("PHY_CLADE", None)
+    else:
+        os.environ["PHY_CLADE"] = str(value)
+    try:
+        return _class_engine(case, max_draws=max_draws)
+    finally:
+        if old is None:
+            os.environ.pop("PHY_CLADE", None)
+        else:
+            os.environ["PHY_CLADE"] = old
+
+
+@pytest.mark.parametrize("seed,S,P,C,model,rooted,cat", [
+    (7, 128, 3000, 4, "GTR", True, False),
+    (9, 300, 500, 4, "GTR", True, False),
+    (4, 17, 257, 5, "GTR", False, False),
+    (5, 40, 200, 2, "GTR", True, True),
+])
+def test_class_clades_bitwise_equal_to_level_launches(seed, S, P, C, model, rooted, cat):
+    """Bottom clades (levels 1..Lc fused, one workgroup per clade) run the
+    same chunks / tiles / spans in the same order as the per-level launches:
+    outputs bitwise equal for the automatic plan and forced depths, and the
+    forced-deepest plan still matches the oracle."""
+    case = cases.random_case(seed, S=S, P=P, C=C, model=model, rooted=rooted, caterpillar=cat)
+    ref_eng = _with_clade(case, 0)
+    assert ref_eng.class_info()["clade_levels"] == 0
+    ref = ref_eng.evaluate(case.blens, case.model_vec(), site_ll=True)
+    levels = ref_eng.class_info()["levels"]
+    for value in (None, 1, 3, levels):
+        eng = _with_clade(case, value)
+        info = eng.class_info()
+        if value is not None:
+            assert info["clade_levels"] == max(0, min(value, levels - 2))
+        got = eng.evaluate(case.blens, case.model_vec(), site_ll=True)
+        assert got.loglik == ref.loglik
+        assert np.array_equal(got.site_ll, ref.site_ll)
+        assert np.array_equal(got.dLdP, ref.dLdP) and np.array_equal(got.grad_blens, ref.grad_blens)
+        assert np.array_equal(got.grad_rates, ref.grad_rates) and np.array_equal(got.grad_freqs, ref.grad_freqs)
+    check_case(case, _with_clade(case, levels))
+
+
+def test_class_clades_repetitive_alignment_bitwise():
+    """Long tile-crossing segments inside the fused levels (FIX phases inside
+    the clade workgroups)."""
+    rng = np.random.default_rng(70)
+    base = cases.random_case(70, S=48, P=5000, C=4, model="GTR")
+    codes = np.where(rng.random((48, 5000)) < 0.9, 1, rng.choice([1, 2, 4, 8, 15], size=(48, 5000)))
+    case = cases.Case("rep", codes.astype(np.uint8), base.weights, base.peel0, True, "GTR", 4, base.blens,
+                      base.freqs, base.rates, base.rs, base.ps)
+    ref = _with_clade(case, 0).evaluate(case.blens, case.model_vec(), site_ll=True)
+    eng = _with_clade(case, 50)
+    assert eng.class_info()["clade_levels"] > 0
+    got = eng.evaluate(case.blens, case.model_vec(), site_ll=True)
+    assert got.loglik == ref.loglik and np.array_equal(got.dLdP, ref.dLdP) and np.array_equal(got.site_ll, ref.site_ll)

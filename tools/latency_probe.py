@@ -1,0 +1,41 @@
+#!/usr/bin/env python
+"""Small-batch latency of one log-lik + gradient evaluation (the NUTS round
+shape: n draws per call, compact rows, host buffers): wall time per call.
+Run on the GPU box, optionally under rocprofv3 --kernel-trace --stats."""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--draws", type=int, default=4)
+    ap.add_argument("--calls", type=int, default=300)
+    ap.add_argument("--workload", default="fluA", choices=["fluA", "HCV", "DS1"])
+    a = ap.parse_args()
+    from phylostan_amd.engine import TreeLikelihood
+    from tests import cases
+    case = {"fluA": cases.fluA_case, "HCV": cases.hcv_case, "DS1": cases.ds1_case}[a.workload]()
+    lik = TreeLikelihood(case.tipcodes, case.weights, case.peel0, case.rooted, case.model, case.C,
+                         max_draws=a.draws)
+    lik.set_output(compact=True)
+    bl = np.stack([case.blens * (1.0 + 0.01 * k) for k in range(a.draws)])
+    mv = np.stack([case.model_vec()] * a.draws)
+    for _ in range(20):
+        lik.evaluate_batch(bl, mv)
+    t0 = time.perf_counter()
+    for _ in range(a.calls):
+        lik.evaluate_batch(bl, mv)
+    dt = (time.perf_counter() - t0) / a.calls
+    print(json.dumps({"workload": a.workload, "draws": a.draws, "us_per_call": dt * 1e6}))
+
+
+if __name__ == "__main__":
+    main()
