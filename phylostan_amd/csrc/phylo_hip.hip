@@ -89,7 +89,10 @@ constexpr int F_VDEEP = 4;  // v is the x child of a both-internal parent
 // reverse loaded a step ahead).
 constexpr int F_NOSTORE = 8;   // this step's a_v is not written to scratch
 constexpr int F_PREVREC = 16;  // the child computed at the previous step is rebuilt, not loaded
-constexpr int RD_MAX = 4;      // deepest rebuild chain: a cherry plus up to 3 one-tip nodes above it
+#ifndef PHY_RD_MAX
+#define PHY_RD_MAX 4
+#endif
+constexpr int RD_MAX = PHY_RD_MAX;  // deepest rebuild chain: a cherry plus up to RD_MAX-1 one-tip nodes above it
 
 // The device copy of the program packs a step into 8 ints (pack_program):
 //   w0 x | y<<16   w1 mx | my<<16   w2 mv | vslot<<16   w3 xslot | yslot<<16
@@ -316,6 +319,10 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* base, ui
 // measured +13% (fluA) / +3% (synthetic) over the default policy, with the
 // stores left at the default (nt or sc1 stores measured no better).
 constexpr int LOAD_NT = 2;
+#ifndef PHY_STORE_AUX
+#define PHY_STORE_AUX 0
+#endif
+constexpr int STORE_AUX = PHY_STORE_AUX;  // cache policy of the moved-partial stores (0: default)
 constexpr uint32_t OOB = 0x40000000u;  // out-of-range offset part (regions are < 2^30 bytes, checked at plan time)
 __device__ __forceinline__ V4 ld_v4(__amdgpu_buffer_rsrc_t srd, uint32_t off, uint32_t half) {
   const auto lo = __builtin_amdgcn_raw_buffer_load_b128(srd, off, 0, LOAD_NT);
@@ -336,8 +343,8 @@ __device__ __forceinline__ void st_v4(__amdgpu_buffer_rsrc_t srd, uint32_t off, 
                  (unsigned)__double2hiint(v.y)};
   const u4 hi = {(unsigned)__double2loint(v.z), (unsigned)__double2hiint(v.z), (unsigned)__double2loint(v.w),
                  (unsigned)__double2hiint(v.w)};
-  __builtin_amdgcn_raw_buffer_store_b128(lo, srd, off, 0, 0);
-  __builtin_amdgcn_raw_buffer_store_b128(hi, srd, off, half, 0);
+  __builtin_amdgcn_raw_buffer_store_b128(lo, srd, off, 0, STORE_AUX);
+  __builtin_amdgcn_raw_buffer_store_b128(hi, srd, off, half, STORE_AUX);
 }
 
 // s_waitcnt vmcnt(0) that the compiler's waitcnt pass sees (an inline-asm
