@@ -447,7 +447,7 @@ def main():
             traffic = None
 
     cpu = cpu_mt = check = None
-    if rank == 0 and not args.no_cpu_baseline:
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:  # the CPU baseline is an N=1 figure
         hinfo = host_cpu_info()
         cpu, cpu_out = cpu_baseline(prob, args.cpu_seconds, info=hinfo)
         # the same port on every host thread this job may use (reported beside it)

@@ -403,6 +403,54 @@ __device__ __forceinline__ V4 tipvec_l(const double* tvec, unsigned b) {
   return {lo.x, lo.y, hi.x, hi.y};
 }
 
+// One matrix record (R 4-vectors): the four columns of P(t), then P t for
+// every extra tip mask (pmat_kernel).  Building the records inside the sweep
+// instead (verdict item 4c) was measured: the extra code in the chunk
+// staging path pushed the K=2 kernel into scratch spills and cost 7 % even
+// when unused, 11 % when used (fluA 6.67 ms against 6.0).
+//   e: the draw's eigensystem record (EIG_LEN doubles), t = r_c b.
+__device__ __forceinline__ void build_record(const double* __restrict__ e, double t, int kind, int R,
+                                             unsigned long long extra, double2* po) {
+  double P[16];
+  if (kind == PHY_JC69) {  // generate_script.py:765-769
+    const double ex = exp(-t / 0.75);
+    const double off = 0.25 - 0.25 * ex, d = 0.25 + 0.75 * ex;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) P[k] = (k % 5 == 0) ? d : off;
+  } else {  // m1 diag(exp(lam t)) m2   (:880)
+    double E[4];
+#pragma unroll
+    for (int l = 0; l < 4; ++l) E[l] = exp(e[EIG_LAM + l] * t);
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        double acc = 0.0;
+#pragma unroll
+        for (int l = 0; l < 4; ++l) acc = fma(e[EIG_M1 + j * 4 + l] * E[l], e[EIG_M2 + l * 4 + k], acc);
+        P[j * 4 + k] = acc;
+      }
+  }
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {  // column j
+    po[2 * j] = make_double2(P[j], P[4 + j]);
+    po[2 * j + 1] = make_double2(P[8 + j], P[12 + j]);
+  }
+  for (int v = 4; v < R; ++v) {
+    const unsigned tm = (unsigned)(extra >> (4 * (v - 4))) & 15u;
+    double r[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      double acc = P[i * 4] * (double)(tm & 1u);
+#pragma unroll
+      for (int j = 1; j < 4; ++j) acc = fma(P[i * 4 + j], (double)((tm >> j) & 1u), acc);
+      r[i] = acc;
+    }
+    po[2 * v] = make_double2(r[0], r[1]);
+    po[2 * v + 1] = make_double2(r[2], r[3]);
+  }
+}
+
 // The sweep.  `prog` is a separate __restrict__ const argument so the
 // backend proves it read-only and uses scalar loads.
 //
@@ -1165,48 +1213,8 @@ __global__ void __launch_bounds__(64) pmat_kernel(PmatArgs a) {
     const int c = idx / nmat, m = idx - c * nmat;
     const int br = a.mat_branch[m];
     double2* po = reinterpret_cast<double2*>(recl + (size_t)lane * rlen);
-    double P[16];
-    {
-      const double* mdl = a.model + (size_t)draw * (10 + 2 * C);
-      const double t = a.blens[(size_t)draw * a.B + br] * mdl[10 + c];
-      if (a.kind == PHY_JC69) {  // generate_script.py:765-769
-        const double ex = exp(-t / 0.75);
-        const double off = 0.25 - 0.25 * ex, d = 0.25 + 0.75 * ex;
-#pragma unroll
-        for (int k = 0; k < 16; ++k) P[k] = (k % 5 == 0) ? d : off;
-      } else {  // m1 diag(exp(lam t)) m2   (:880)
-        double E[4];
-#pragma unroll
-        for (int l = 0; l < 4; ++l) E[l] = exp(e[EIG_LAM + l] * t);
-#pragma unroll
-        for (int j = 0; j < 4; ++j)
-#pragma unroll
-          for (int k = 0; k < 4; ++k) {
-            double acc = 0.0;
-#pragma unroll
-            for (int l = 0; l < 4; ++l) acc = fma(e[EIG_M1 + j * 4 + l] * E[l], e[EIG_M2 + l * 4 + k], acc);
-            P[j * 4 + k] = acc;
-          }
-      }
-    }
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {  // column j
-      po[2 * j] = make_double2(P[j], P[4 + j]);
-      po[2 * j + 1] = make_double2(P[8 + j], P[12 + j]);
-    }
-    for (int v = 4; v < a.R; ++v) {
-      const unsigned t = (unsigned)(a.extra >> (4 * (v - 4))) & 15u;
-      double r[4];
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        double acc = P[i * 4] * (double)(t & 1u);
-#pragma unroll
-        for (int j = 1; j < 4; ++j) acc = fma(P[i * 4 + j], (double)((t >> j) & 1u), acc);
-        r[i] = acc;
-      }
-      po[2 * v] = make_double2(r[0], r[1]);
-      po[2 * v + 1] = make_double2(r[2], r[3]);
-    }
+    const double* mdl = a.model + (size_t)draw * (10 + 2 * C);
+    build_record(e, a.blens[(size_t)draw * a.B + br] * mdl[10 + c], a.kind, a.R, a.extra, po);
   }
   __syncthreads();
   const double2* src = reinterpret_cast<const double2*>(recl);
@@ -2180,6 +2188,7 @@ int phy_create(int S, int P, int C, int rooted, int model, const uint8_t* tipcod
     c->recompute = rk ? atoi(rk) != 0 : true;
     const char* fk = getenv("PHY_FIN");
     c->fin_pref = fk ? atoi(fk) != 0 : true;
+
   }
   hipError_t he = hipSetDevice(device);
   if (he != hipSuccess) {

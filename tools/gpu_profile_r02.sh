@@ -7,6 +7,8 @@ TAG=${1:-r02}
 O=gpurun_out/prof_$TAG; mkdir -p $O
 timeout -k 10 200 python tools/pmc_traffic.py --workload fluA --engine pattern --scratch $O/pmc > $O/pmc_fluA.log 2>&1 && \
 timeout -k 10 300 python tools/pmc_traffic.py --workload synthetic --engine class --scratch $O/pmc > $O/pmc_syn.log 2>&1 && \
+timeout -k 10 200 python tools/pmc_traffic.py --workload HCV --engine pattern --scratch $O/pmc > $O/pmc_HCV.log 2>&1 && \
+timeout -k 10 200 python tools/pmc_traffic.py --workload DS1 --engine pattern --scratch $O/pmc > $O/pmc_DS1.log 2>&1 && \
 cp profiles/pmc_traffic.json $O/pmc_traffic.json && \
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/rp_fluA -o run --output-format csv -- python bench.py --no-cpu-baseline --json-out $O/fluA_under_rocprof.json > $O/fluA_rp.log 2>&1 && \
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/rp_syn -o run --output-format csv -- python bench.py --workload synthetic --steps 20 --warmup 3 --no-cpu-baseline --json-out $O/syn_under_rocprof.json > $O/syn_rp.log 2>&1 && \

@@ -64,7 +64,7 @@ def main():
     ap.add_argument("--scratch", default=os.path.join(ROOT, "gpurun_out", "pmc"))
     args = ap.parse_args()
     from bench import kernel_source_hash
-    draws = args.draws or (8192 if args.workload == "fluA" else 1)
+    draws = args.draws or (1 if args.workload == "synthetic" else 8192)
     bench_args = ["--workload", args.workload, "--draws", str(draws), "--steps", "3", "--warmup", "1",
                   "--no-cpu-baseline", "--engine", args.engine]
     tag = "%s_%s" % (args.workload, args.engine)
