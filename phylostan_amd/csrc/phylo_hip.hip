@@ -89,6 +89,9 @@ constexpr int F_VDEEP = 4;  // v is the x child of a both-internal parent
 // reverse loaded a step ahead).
 constexpr int F_NOSTORE = 8;   // this step's a_v is not written to scratch
 constexpr int F_PREVREC = 16;  // the child computed at the previous step is rebuilt, not loaded
+#ifndef PHY_EPI_U
+#define PHY_EPI_U 4  // dL/dP slot items in flight per lane in the per-draw epilogue
+#endif
 #ifndef PHY_RD_MAX
 #define PHY_RD_MAX 4
 #endif
@@ -999,7 +1002,7 @@ __global__ void __launch_bounds__(MAXT) __attribute__((amdgpu_waves_per_eu(K == 
     const int e16 = lane & 15, j = e16 >> 2, kk = e16 & 3;
     const double q0 = Qd[j * 4 + 0], q1 = Qd[j * 4 + 1], q2 = Qd[j * 4 + 2], q3 = Qd[j * 4 + 3];
     const int tot = nmat * 16;  // a multiple of 16: 16-lane groups are whole
-    constexpr int U = 4;
+    constexpr int U = PHY_EPI_U;
     for (int k0 = lane; k0 < tot; k0 += WAVE * U) {
       double g[U], qp[U];
       int bb[U];
@@ -2110,6 +2113,29 @@ int launch_pattern(phy_ctx* ctx, int n, const double* d_blens, const double* d_m
   return PHY_OK;
 }
 
+// Per-workgroup regions of the pattern sweep for `cap` workgroup slots:
+// moved-partial scratch, global deep entries, dL/dP and scalar slots.
+int alloc_wg_buffers(phy_ctx* c, long cap) {
+  double2** d2[] = {&c->d_scratch, &c->d_dstk};
+  for (double2** b : d2)
+    if (*b) {
+      (void)hipFree(*b);
+      *b = nullptr;
+    }
+  double** d1[] = {&c->d_gslot, &c->d_sslot};
+  for (double** b : d1)
+    if (*b) {
+      (void)hipFree(*b);
+      *b = nullptr;
+    }
+  const size_t ncolwg = (size_t)c->C * WAVE;
+  int rc = dalloc(&c->d_scratch, (size_t)cap * std::max(c->nslots, 1) * 2 * 2 * ncolwg);
+  if (!rc) rc = dalloc(&c->d_dstk, (size_t)cap * std::max(c->ndeep, 1) * 2 * 2 * ncolwg);
+  if (!rc) rc = dalloc(&c->d_gslot, (size_t)cap * c->C * c->nmat * 16);
+  if (!rc) rc = dalloc(&c->d_sslot, (size_t)cap * c->C * 8);
+  return rc;
+}
+
 }  // namespace
 
 extern "C" {
@@ -2246,10 +2272,7 @@ int phy_create(int S, int P, int C, int rooted, int model, const uint8_t* tipcod
   TRY_C(dalloc(&c->d_blens, (size_t)max_draws * c->B));
   TRY_C(dalloc(&c->d_out, (size_t)max_draws * phy_output_len(c)));
   TRY_C(dalloc(&c->d_site, (size_t)max_draws * P));
-  TRY_C(dalloc(&c->d_scratch, (size_t)c->wg_cap * std::max(c->nslots, 1) * 2 * 2 * ncolwg));
-  TRY_C(dalloc(&c->d_dstk, (size_t)c->wg_cap * std::max(c->ndeep, 1) * 2 * 2 * ncolwg));
-  TRY_C(dalloc(&c->d_gslot, (size_t)c->wg_cap * C * c->nmat * 16));
-  TRY_C(dalloc(&c->d_sslot, (size_t)c->wg_cap * C * 8));
+  TRY_C(alloc_wg_buffers(c, c->wg_cap));
   {
     // tip nibbles: record vector of the pattern's mask (R <= 16); padding =
     // mask 15; pattern 2j in the low nibble of byte j, 2j+1 in the high one
@@ -2417,7 +2440,13 @@ int phy_set_tuning(phy_ctx* ctx, int wg_budget, int cols, int lds_budget) {
   if (wg_budget > 0) {
     const long need = std::min<long>((long)nblk_for(ctx->P, 1) * ctx->max_draws,
                                      (long)std::max(wg_budget, 4 * ctx->cu_count) + ctx->max_draws);
-    if (need > ctx->wg_cap) return fail(PHY_ERANGE, "wg_budget larger than allocated at create");
+    if (need > ctx->wg_cap) {  // grow the per-workgroup regions (after the stream's work drains)
+      HIP_TRY(hipSetDevice(ctx->device));
+      HIP_TRY(hipStreamSynchronize(ctx->stream));
+      int rc = alloc_wg_buffers(ctx, need);
+      if (rc) return rc;
+      ctx->wg_cap = (int)need;
+    }
     ctx->wg_budget = wg_budget;
   }
   if (cols < 0 || cols > 2) return fail(PHY_EINVAL, "cols must be 0 (automatic), 1 or 2");

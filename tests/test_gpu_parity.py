@@ -376,3 +376,17 @@ def test_compact_output_rows(engine):
         for k in ("grad_blens", "grad_rs", "grad_ps", "grad_freq_root", "grad_rates", "grad_freqs"):
             np.testing.assert_array_equal(getattr(a, k), getattr(b, k))
     check_case(case, eng.__class__(case.tipcodes, case.weights, case.peel0, case.rooted, case.model, case.C))
+
+
+def test_tuning_grows_workgroup_regions_past_create():
+    """phy_set_tuning with a workgroup budget beyond what phy_create sized
+    the per-workgroup regions for grows them (round 1 refused with
+    PHY_ERANGE); results equal the default plan's."""
+    case = cases.random_case(91, S=30, P=5000, C=4, model="GTR")
+    eng = _engine(case, max_draws=2)
+    ref = eng.evaluate(case.blens, case.model_vec(), site_ll=True)
+    eng.set_tuning(4096, 1, 0)  # 1 column per lane: up to 79 blocks per draw
+    got = eng.evaluate(case.blens, case.model_vec(), site_ll=True)
+    np.testing.assert_allclose(got.site_ll, ref.site_ll, rtol=RTOL_LL, atol=1e-12)
+    _close(got.dLdP, ref.dLdP, RTOL_G, "dLdP")
+    check_case(case, eng, got)
