@@ -1570,6 +1570,12 @@ struct phy_ctx {
   double* d_blens = nullptr;
   double* d_out = nullptr;
   double* d_site = nullptr;
+  // small host-buffer evaluations (phy_eval with n <= PIN_DRAWS): inputs packed
+  // into one pinned staging buffer and one device buffer (one H2D copy), the
+  // output rows back through pinned memory (asynchronous DMA both ways)
+  double* h_in = nullptr;   // pinned [PIN_DRAWS][B + model_len]
+  double* h_out = nullptr;  // pinned [PIN_DRAWS][full output row]
+  double* d_in = nullptr;   // device [PIN_DRAWS][B + model_len]
   double2* d_scratch = nullptr;
   double2* d_dstk = nullptr;
   double* d_gslot = nullptr;
@@ -1590,9 +1596,11 @@ void free_ctx(phy_ctx* c) {
   (void)hipSetDevice(c->device);
   void* ptrs[] = {c->d_tips,  c->d_w,     c->d_prog,    c->d_gpos,    c->d_mat_branch, c->d_pmat,
                   c->d_eig,   c->d_inner, c->d_model,   c->d_blens,   c->d_out,        c->d_site,
-                  c->d_scratch, c->d_dstk, c->d_gslot,  c->d_sslot, c->d_grows};
+                  c->d_scratch, c->d_dstk, c->d_gslot,  c->d_sslot, c->d_grows, c->d_in};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
+  if (c->h_in) (void)hipHostFree(c->h_in);
+  if (c->h_out) (void)hipHostFree(c->h_out);
   for (hipEvent_t e : c->ev) (void)hipEventDestroy(e);
   free_class_engine(c->ce);
   if (c->stream) (void)hipStreamDestroy(c->stream);
@@ -1789,6 +1797,7 @@ int dalloc(T** p, size_t n) {
 #include "class_engine.inc"
 
 constexpr size_t LDS_CAP = 160 * 1024;
+constexpr int PIN_DRAWS = 64;  // phy_eval batches up to this size go through pinned staging
 constexpr int MIN_CAP = 24;  // an occupancy level is taken only if chunks stay this large
 
 int nblk_for(int P, int K) { return (P + WAVE * K - 1) / (WAVE * K); }
@@ -2274,6 +2283,13 @@ int phy_create(int S, int P, int C, int rooted, int model, const uint8_t* tipcod
   TRY_C(dalloc(&c->d_site, (size_t)max_draws * P));
   TRY_C(alloc_wg_buffers(c, c->wg_cap));
   {
+    const size_t pin = (size_t)std::min(max_draws, PIN_DRAWS);
+    const size_t outlen_full = (size_t)1 + c->B + 2 * C + 14 + (size_t)16 * C * c->B;
+    TRY_C(dalloc(&c->d_in, pin * (c->B + 10 + 2 * C)));
+    HIP_C(hipHostMalloc((void**)&c->h_in, sizeof(double) * pin * (c->B + 10 + 2 * C), hipHostMallocDefault));
+    HIP_C(hipHostMalloc((void**)&c->h_out, sizeof(double) * pin * outlen_full, hipHostMallocDefault));
+  }
+  {
     // tip nibbles: record vector of the pattern's mask (R <= 16); padding =
     // mask 15; pattern 2j in the low nibble of byte j, 2j+1 in the high one
     const int row = c->Ppad / 2;
@@ -2374,6 +2390,21 @@ int phy_eval(phy_ctx* ctx, int n_draws, const double* blens, const double* model
   HIP_TRY(hipSetDevice(ctx->device));
   hipStream_t st = ctx->stream;
   const int ml = 10 + 2 * ctx->C;
+  if (n_draws <= PIN_DRAWS && ctx->h_in && ctx->h_out && ctx->d_in) {  // the small-batch (sampler) path
+    const size_t nb = (size_t)n_draws * ctx->B, nm = (size_t)n_draws * ml;
+    const size_t no = (size_t)n_draws * phy_output_len(ctx);
+    std::memcpy(ctx->h_in, blens, sizeof(double) * nb);
+    std::memcpy(ctx->h_in + nb, model, sizeof(double) * nm);
+    HIP_TRY(hipMemcpyAsync(ctx->d_in, ctx->h_in, sizeof(double) * (nb + nm), hipMemcpyHostToDevice, st));
+    int rc = launch(ctx, n_draws, ctx->d_in, ctx->d_in + nb, ctx->d_out, site_ll ? ctx->d_site : nullptr, st);
+    if (rc) return rc;
+    HIP_TRY(hipMemcpyAsync(ctx->h_out, ctx->d_out, sizeof(double) * no, hipMemcpyDeviceToHost, st));
+    if (site_ll)
+      HIP_TRY(hipMemcpyAsync(site_ll, ctx->d_site, sizeof(double) * n_draws * ctx->P, hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    std::memcpy(out, ctx->h_out, sizeof(double) * no);
+    return PHY_OK;
+  }
   HIP_TRY(hipMemcpyAsync(ctx->d_blens, blens, sizeof(double) * n_draws * ctx->B, hipMemcpyHostToDevice, st));
   HIP_TRY(hipMemcpyAsync(ctx->d_model, model, sizeof(double) * n_draws * ml, hipMemcpyHostToDevice, st));
   int rc = launch(ctx, n_draws, ctx->d_blens, ctx->d_model, ctx->d_out, site_ll ? ctx->d_site : nullptr, st);

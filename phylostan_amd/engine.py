@@ -131,6 +131,19 @@ class TreeLikelihood:
                                      _ptr(sl) if site_ll else None), "phy_eval")
         return [EvalResult(out[k], self.B, self.C, sl[k] if site_ll else None) for k in range(n)]
 
+    def evaluate_rows(self, blens, model_vecs):
+        """n draws -> the raw output rows [n, outlen] (no per-draw objects:
+        the sampler's path)."""
+        blens = np.ascontiguousarray(np.atleast_2d(blens), dtype=np.float64)
+        mv = np.ascontiguousarray(np.atleast_2d(model_vecs), dtype=np.float64)
+        n = blens.shape[0]
+        if blens.shape != (n, self.B) or mv.shape != (n, self.model_len):
+            raise ValueError("bad shapes: blens %s model %s" % (blens.shape, mv.shape))
+        out = np.empty((n, self.outlen))
+        _lib.check(self.lib.phy_eval(self.ctx, n, blens.ctypes.data, mv.ctypes.data, out.ctypes.data, None),
+                   "phy_eval")
+        return out
+
     def evaluate(self, blens, model_vec, site_ll=False):
         return self.evaluate_batch(blens, model_vec, site_ll)[0]
 

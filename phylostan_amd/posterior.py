@@ -351,6 +351,14 @@ class Posterior:
             return rs, ps
         return np.ones((n, 1)), np.ones((n, 1))
 
+    def _lik_rows(self, blens, mv, width):
+        """The likelihood's compact output rows [n, width] (the engine's raw
+        rows when it offers them, else assembled from EvalResult objects)."""
+        if hasattr(self.lik, "evaluate_rows"):
+            return self.lik.evaluate_rows(blens, mv)[:, :width]
+        return np.stack([np.concatenate([[r.loglik], r.grad_blens, r.grad_rs, r.grad_ps, r.grad_freq_root,
+                                         r.grad_rates, r.grad_freqs]) for r in self.lik.evaluate_batch(blens, mv)])
+
     def _heights(self, vals, n):
         if self._nat is not None:
             return self._nat.heights(vals["props"], vals["height"])
@@ -518,14 +526,15 @@ class Posterior:
         mv = np.concatenate([freqs, R, rs, ps], axis=1)
         ok = (np.isfinite(lp) & np.all(np.isfinite(mv), axis=1) & np.all(np.isfinite(blens), axis=1)
               & np.all(freqs > 0, axis=1))
-        ll = np.full(n, -np.inf)
-        res = [None] * n
+        # compact output rows (include/phylo_hip.h): [ll, d/dblens, d/drs, d/dps,
+        # d/dfreqs root term, d/d exchangeabilities, d/dfreqs]; zeros where not evaluated
+        o = 1 + self.B + 2 * C
+        rows = np.zeros((n, o + 14))
+        rows[:, 0] = -np.inf
         if ok.any():
             sel = np.nonzero(ok)[0]
-            out = self.lik.evaluate_batch(blens[sel], mv[sel])
-            for k, r in zip(sel, out):
-                res[k] = r
-                ll[k] = r.loglik
+            rows[sel] = self._lik_rows(blens[sel], mv[sel], o + 14)
+        ll = rows[:, 0]
         lp = lp + ll
         bad = ~np.isfinite(lp)
 
@@ -601,16 +610,15 @@ class Posterior:
             return lp, None
 
         # ---- likelihood gradient -> constrained parameters
-        zb, zc = np.zeros(self.B), np.zeros(C)
-        g_bl = np.stack([r.grad_blens if r is not None else zb for r in res])
-        g_rs = np.stack([r.grad_rs if r is not None else zc for r in res])
-        g_ps = np.stack([r.grad_ps if r is not None else zc for r in res])
+        g_bl = rows[:, 1:1 + self.B]
+        g_rs = rows[:, 1 + self.B:1 + self.B + C]
+        g_ps = rows[:, 1 + self.B + C:o]
         if sp.model != "JC69":
             # the engine's chain rule through Q's eigendecomposition (include/phylo_hip.h)
             good = np.nonzero(~bad)[0]
             if len(good):
-                gr = np.stack([res[d].grad_rates for d in good])
-                gf = np.stack([res[d].grad_freqs for d in good])
+                gr = rows[good, o + 4:o + 10]
+                gf = rows[good, o + 10:o + 14]
                 gx["freqs"][good] += gf
                 if sp.model == "GTR":
                     gx["rates"][good] += gr
