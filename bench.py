@@ -53,8 +53,9 @@ def parse():
     ap.add_argument("--wg-budget", type=int, default=0)
     ap.add_argument("--cols", type=int, default=0, help="pattern columns per lane (0 = automatic)")
     ap.add_argument("--lds-budget", type=int, default=0)
-    ap.add_argument("--engine", choices=["auto", "pattern", "class"], default="auto",
-                    help="pattern sweep, class sweep (site repeats) or the context's automatic choice")
+    ap.add_argument("--engine", choices=["auto", "pattern", "class", "resident"], default="auto",
+                    help="pattern sweep, class sweep (site repeats), resident class sweep (per draw-category "
+                         "state in LDS) or the context's automatic choice")
     ap.add_argument("--json-out", default=None)
     ap.add_argument("--shard-of", type=int, default=0,
                     help="synthetic: evaluate only the first of this many pattern shards on one GPU, with no "
@@ -68,7 +69,7 @@ def parse():
 
 def kernel_source_hash():
     h = hashlib.sha1()
-    for name in ("phylo_hip.hip", "class_engine.inc"):
+    for name in ("phylo_hip.hip", "class_engine.inc", "resident_engine.inc"):
         with open(os.path.join(ROOT, "phylostan_amd", "csrc", name), "rb") as fp:
             h.update(fp.read())
     return h.hexdigest()[:12]
@@ -155,6 +156,17 @@ def class_algorithmic_bytes(C, classes, stage, staged, draws):
     (secondary children) are also stored and read back by the segmented
     reduction -- 2 x 32 B more (a primary child's are reduced in registers)."""
     return 32 * C * (3 * classes + 2 * stage + 2 * staged) * draws
+
+
+def resident_algorithmic_bytes(C, B, root_classes, record_vectors, draws):
+    """HBM bytes of one resident-class-sweep launch pair: per
+    (draw, category) the matrix records are read by both kernels (32 B per
+    vector), ps_c pi.p_root written once per root class and read by every
+    category's reverse (C reads), the B dL/dP rows written (128 B each), the
+    scalar slot; per draw log L per root class.  Moved and upper partials
+    never leave LDS."""
+    per_dc = 2 * 32 * record_vectors + 8 * root_classes * (1 + C) + 128 * B + 64
+    return (C * per_dc + 8 * root_classes) * draws
 
 
 def survey_bytes(S, P, C, draws):
@@ -325,6 +337,8 @@ def main():
     info["engine"] = eng.engine()
     if info["engine"] == "class":
         info.update({"class_" + k: v for k, v in eng.class_info().items()})
+    if info["engine"] == "resident":
+        info.update({"resident_" + k: v for k, v in eng.resident_info().items()})
     B = eng.B
     P_local = sl.p1 - sl.p0
 
@@ -430,6 +444,10 @@ def main():
     if info["engine"] == "class":
         alg = class_algorithmic_bytes(C, info["class_classes"], info["class_stage"], info["class_staged"], draws)
         kernel_name = "class sweep: cls_fwd/cls_root/cls_red/cls_fix/cls_rev kernels, forward through reverse"
+    elif info["engine"] == "resident":
+        alg = resident_algorithmic_bytes(C, B, info["resident_root_classes"], info["resident_record_vectors"],
+                                         draws)
+        kernel_name = "resident class sweep: res_fwd_kernel + res_rev_kernel"
     else:
         alg = algorithmic_bytes(S, P_local, C, info["nslots"] - info.get("recomputed", 0), B, draws)
         kernel_name = "sweep_kernel"

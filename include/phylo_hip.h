@@ -206,6 +206,13 @@ int phy_class_info(const phy_ctx* ctx, long long* classes, int* levels, int* roo
  * Results are bitwise the same either way. */
 int phy_class_clades(const phy_ctx* ctx, int* fused_levels, int* clades, long long* largest);
 
+/* Resident class sweep plan (engine 3; zeros when none is built): LDS bytes
+ * of one (draw, category) workgroup, non-root classes, levels, root classes,
+ * reverse chunks of 16 classes (their dL/dP partials are summed in LDS) and
+ * matrix-record vectors staged per (draw, category). */
+int phy_resident_info(const phy_ctx* ctx, int* lds_bytes, long long* classes, int* levels, int* root_classes,
+                      int* partials, int* record_vectors);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1529,6 +1529,8 @@ __global__ void __launch_bounds__(256) qgrad_kernel(FinArgs a) {
 namespace {
 struct ClassEngine;  // class_engine.inc
 void free_class_engine(ClassEngine* e);
+struct ResEngine;  // resident_engine.inc
+void free_res_engine(ResEngine* e);
 }  // namespace
 
 struct phy_ctx {
@@ -1547,9 +1549,12 @@ struct phy_ctx {
   bool fin_pref = true;        // finalize inside the sweep when one workgroup runs a draw (PHY_FIN=0: off)
   int nrec = 0;                // cherries recomputed under the current plan
   // engine: 0 = pattern sweep (sweep_kernel), 1 = class sweep (site repeats,
-  // class_engine.inc); engine_pref 0 = automatic, 1 = pattern, 2 = class
+  // class_engine.inc), 2 = resident class sweep (resident_engine.inc);
+  // engine_pref 0 = automatic, 1 = pattern, 2 = class, 3 = resident
   int engine = 0, engine_pref = 0;
   ClassEngine* ce = nullptr;
+  ResEngine* re = nullptr;
+  bool re_tried = false;       // the resident plan was built (or found not to apply)
   int compact = 0;             // output rows without the dL/dP block (phy_set_output)
   double* d_grows = nullptr;   // dL/dP rows when compact: [max_draws][16 C B]
   std::vector<uint8_t> h_tips;  // host copies of the static data (the class plan is built on demand)
@@ -1603,6 +1608,7 @@ void free_ctx(phy_ctx* c) {
   if (c->h_out) (void)hipHostFree(c->h_out);
   for (hipEvent_t e : c->ev) (void)hipEventDestroy(e);
   free_class_engine(c->ce);
+  free_res_engine(c->re);
   if (c->stream) (void)hipStreamDestroy(c->stream);
   (void)hipSetDevice(dev_old);
   delete c;
@@ -1797,6 +1803,8 @@ int dalloc(T** p, size_t n) {
 #include "class_engine.inc"
 
 constexpr size_t LDS_CAP = 160 * 1024;
+
+#include "resident_engine.inc"
 constexpr int PIN_DRAWS = 64;  // phy_eval batches up to this size go through pinned staging
 constexpr int MIN_CAP = 24;  // an occupancy level is taken only if chunks stay this large
 
@@ -1934,9 +1942,24 @@ int ensure_class_plan(phy_ctx* c) {
                             c->vec_of, c->R, c->nmat, c->gpos, &c->ce);
 }
 
+int ensure_res_plan(phy_ctx* c) {
+  if (c->re_tried) return PHY_OK;
+  c->re_tried = true;
+  return build_res_engine(c->S, c->P, c->C, c->rooted, c->h_tips.data(), c->h_w.data(), c->h_peel.data(),
+                          c->vec_of, c->R, c->nmat, c->gpos, LDS_CAP, &c->re);
+}
+
 int select_engine(phy_ctx* c) {
   c->engine = 0;
   if (c->engine_pref == 1) return PHY_OK;
+  if (c->engine_pref == 3) {
+    int rc = ensure_res_plan(c);
+    if (rc) return rc;
+    if (!c->re) return fail(PHY_EINVAL, "resident class sweep: needs a rooted tree whose per-(draw, category) "
+                                        "class state fits in LDS");
+    c->engine = 2;
+    return PHY_OK;
+  }
   if (c->engine_pref == 0 && c->P < 16384) return PHY_OK;
   int rc = ensure_class_plan(c);
   if (rc) return rc;
@@ -2047,6 +2070,35 @@ int launch_class(phy_ctx* ctx, int n, const double* d_blens, const double* d_mod
 int launch_pattern(phy_ctx* ctx, int n, const double* d_blens, const double* d_model, double* d_out,
                    double* d_site, hipStream_t st, double* grows, long long gstride);
 
+// The resident class sweep (resident_engine.inc): forward + root L, then the
+// forward again with the reverse, one workgroup per (draw, category) each
+// (the reverse writes the dL/dP rows itself); the shared finalize.  The
+// timed region spans the two sweep kernels.
+int launch_res(phy_ctx* ctx, int n, const double* d_blens, const double* d_model, double* d_out,
+               double* d_site, hipStream_t st, double* grows, long long gstride) {
+  ResEngine* e = ctx->re;
+  const int C = ctx->C, B = ctx->B;
+  int rc = res_engine_reserve(e, n);
+  if (rc) return rc;
+  const ResArgs a = res_args(e, ctx->d_pmat, d_model, ctx->extra, grows, gstride);
+  const int dcn = n * C;
+  hipEvent_t e0 = nullptr, e1 = nullptr;
+  if (ctx->timing && (rc = timing_begin(ctx, st, &e0, &e1))) return rc;
+  hipLaunchKernelGGL(res_fwd_kernel, dim3(dcn), dim3(RES_THREADS), e->lds, st, a);
+  hipLaunchKernelGGL(res_rev_kernel, dim3(dcn), dim3(RES_THREADS), e->lds, st, a);
+  HIP_TRY(hipGetLastError());
+  if (ctx->timing) HIP_TRY(hipEventRecord(e1, st));
+  if (d_site)
+    hipLaunchKernelGGL(cls_site_kernel, dim3((ctx->P + 255) / 256, n), dim3(256), 0, st,
+                       (const double*)e->d_sitecls, (const int*)e->d_pat_root, d_site, ctx->P, e->nroot);
+  FinArgs fa{ctx->d_gslot, e->d_sslot, ctx->d_pmat, ctx->d_eig, d_blens, d_model, ctx->d_gpos, ctx->d_inner, d_out,
+             C,            B,          ctx->nmat,   1,           phy_output_len(ctx), 0, ctx->R, grows, gstride,
+             ctx->kind};
+  hipLaunchKernelGGL(finalize_kernel, dim3(n), dim3(256), ((size_t)C * B + 16 + 256) * sizeof(double), st, fa);
+  HIP_TRY(hipGetLastError());
+  return PHY_OK;
+}
+
 int launch(phy_ctx* ctx, int n, const double* d_blens, const double* d_model, double* d_out,
            double* d_site, hipStream_t st) {
   const int C = ctx->C, B = ctx->B;
@@ -2061,8 +2113,9 @@ int launch(phy_ctx* ctx, int n, const double* d_blens, const double* d_model, do
   }
   double* grows = ctx->compact ? ctx->d_grows : d_out + PHY_OUT_G(B, C);
   const long long gstride = ctx->compact ? (long long)16 * C * B : (long long)phy_output_len(ctx);
-  int rc0 = ctx->engine == 1 ? launch_class(ctx, n, d_blens, d_model, d_out, d_site, st, grows, gstride)
-                             : launch_pattern(ctx, n, d_blens, d_model, d_out, d_site, st, grows, gstride);
+  int rc0 = ctx->engine == 1   ? launch_class(ctx, n, d_blens, d_model, d_out, d_site, st, grows, gstride)
+            : ctx->engine == 2 ? launch_res(ctx, n, d_blens, d_model, d_out, d_site, st, grows, gstride)
+                               : launch_pattern(ctx, n, d_blens, d_model, d_out, d_site, st, grows, gstride);
   if (rc0) return rc0;
   FinArgs qa{ctx->d_gslot, ctx->d_sslot, ctx->d_pmat, ctx->d_eig, d_blens, d_model, ctx->d_gpos, ctx->d_inner, d_out,
              C,            B,            ctx->nmat,   1,           phy_output_len(ctx), 0, ctx->R, grows, gstride,
@@ -2244,6 +2297,8 @@ int phy_create(int S, int P, int C, int rooted, int model, const uint8_t* tipcod
     const void* ks[] = {(const void*)sweep_kernel<1024, 1, false>, (const void*)sweep_kernel<512, 2, false>,
                         (const void*)sweep_kernel<1024, 1, true>, (const void*)sweep_kernel<512, 2, true>};
     for (const void* k : ks) (void)hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)LDS_CAP);
+    (void)hipFuncSetAttribute((const void*)res_fwd_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)LDS_CAP);
+    (void)hipFuncSetAttribute((const void*)res_rev_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)LDS_CAP);
   }
   if (lds_bytes(S, C, c->R, 3, 1, 0) > LDS_CAP) {
     delete c;
@@ -2332,7 +2387,7 @@ int phy_create(int S, int P, int C, int rooted, int model, const uint8_t* tipcod
   c->vec_of = vec_of;
   {
     const char* ek = getenv("PHY_ENGINE");
-    c->engine_pref = ek ? std::max(0, std::min(2, atoi(ek))) : 0;
+    c->engine_pref = ek ? std::max(0, std::min(3, atoi(ek))) : 0;
   }
   TRY_C(select_engine(c));
   *out = c;
@@ -2508,7 +2563,8 @@ int phy_recomputed_partials(const phy_ctx* ctx) { return ctx ? ctx->nrec : -1; }
 
 int phy_set_engine(phy_ctx* ctx, int mode) {
   if (!ctx) return fail(PHY_EINVAL, "NULL ctx");
-  if (mode < 0 || mode > 2) return fail(PHY_EINVAL, "engine must be 0 (automatic), 1 (pattern) or 2 (class)");
+  if (mode < 0 || mode > 3)
+    return fail(PHY_EINVAL, "engine must be 0 (automatic), 1 (pattern), 2 (class) or 3 (resident)");
   HIP_TRY(hipSetDevice(ctx->device));
   HIP_TRY(hipStreamSynchronize(ctx->stream));
   ctx->engine_pref = mode;
@@ -2542,6 +2598,19 @@ int phy_class_clades(const phy_ctx* ctx, int* fused_levels, int* clades, long lo
   if (fused_levels) *fused_levels = e ? e->Lc : 0;
   if (clades) *clades = e ? e->nclade : 0;
   if (largest) *largest = e ? e->clade_max : 0;
+  return PHY_OK;
+}
+
+int phy_resident_info(const phy_ctx* ctx, int* lds_bytes, long long* classes, int* levels, int* root_classes,
+                      int* partials, int* record_vectors) {
+  if (!ctx) return fail(PHY_EINVAL, "NULL ctx");
+  const ResEngine* e = ctx->re;
+  if (lds_bytes) *lds_bytes = e ? (int)e->lds : 0;
+  if (classes) *classes = e ? e->classes : 0;
+  if (levels) *levels = e ? e->L : 0;
+  if (root_classes) *root_classes = e ? e->nroot : 0;
+  if (partials) *partials = e ? e->nchunks : 0;
+  if (record_vectors) *record_vectors = e ? e->nmc : 0;
   return PHY_OK;
 }
 

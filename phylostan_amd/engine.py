@@ -201,14 +201,15 @@ class TreeLikelihood:
         self.outlen = self.lib.phy_output_len(self.ctx)
 
     def set_engine(self, mode=0):
-        """0 automatic, 1 pattern sweep, 2 class sweep (site repeats)."""
+        """0 automatic, 1 pattern sweep, 2 class sweep (site repeats), 3 resident
+        class sweep (the class sweep with each draw-category's state in LDS)."""
         if isinstance(mode, str):
-            mode = {"auto": 0, "pattern": 1, "class": 2}[mode]
+            mode = {"auto": 0, "pattern": 1, "class": 2, "resident": 3}[mode]
         _lib.check(self.lib.phy_set_engine(self.ctx, int(mode)), "phy_set_engine")
 
     def engine(self):
-        """The engine the next launch uses: "pattern" or "class"."""
-        return ("pattern", "class")[self.lib.phy_engine(self.ctx)]
+        """The engine the next launch uses: "pattern", "class" or "resident"."""
+        return ("pattern", "class", "resident")[self.lib.phy_engine(self.ctx)]
 
     def class_info(self):
         ll = [ctypes.c_longlong() for _ in range(3)]
@@ -222,6 +223,16 @@ class TreeLikelihood:
         return dict(classes=ll[0].value, levels=ii[0].value, root_classes=ii[1].value, stage=ll[1].value,
                     staged=ll[2].value, tiles=ii[2].value, spans=ii[3].value, clade_levels=fl.value,
                     clades=nc.value, clade_max=big.value)
+
+    def resident_info(self):
+        """The resident class sweep's plan (zeros when it has none)."""
+        ii = [ctypes.c_int() for _ in range(5)]
+        cl = ctypes.c_longlong()
+        _lib.check(self.lib.phy_resident_info(self.ctx, ctypes.byref(ii[0]), ctypes.byref(cl), ctypes.byref(ii[1]),
+                                              ctypes.byref(ii[2]), ctypes.byref(ii[3]), ctypes.byref(ii[4])),
+                   "phy_resident_info")
+        return dict(lds_bytes=ii[0].value, classes=cl.value, levels=ii[1].value, root_classes=ii[2].value,
+                    partials=ii[3].value, record_vectors=ii[4].value)
 
     def timing_start(self):
         _lib.check(self.lib.phy_timing_start(self.ctx), "phy_timing_start")

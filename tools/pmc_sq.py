@@ -35,18 +35,22 @@ def main():
         # sum over one evaluation's cls_* dispatches (evaluations counted by
         # cls_root_ll_kernel)
         cls = "class" in bench_args
+        only = os.environ.get("PMC_KERNEL")  # e.g. res_rev_kernel: that kernel's dispatches only
         acc, nev = {}, {}
         for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
             for row in csv.DictReader(open(f)):
                 name = row["Kernel_Name"]
-                if cls:
+                if only:
+                    if only not in name:
+                        continue
+                elif cls:
                     if "cls_" not in name or "gsum" in name or "site" in name:
                         continue
                 elif "sweep_kernel" not in name:
                     continue
                 cn = row["Counter_Name"]
                 acc[cn] = acc.get(cn, 0.0) + float(row["Counter_Value"])
-                if not cls or "cls_root_ll_kernel" in name:
+                if only or not cls or "cls_root_ll_kernel" in name:
                     nev[cn] = nev.get(cn, 0) + 1
         for cn, v in acc.items():
             out[cn] = v / max(nev.get(cn, 1), 1)
