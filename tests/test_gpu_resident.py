@@ -36,7 +36,7 @@ def test_resident_config_datasets(make):
     (5, 40, 90, 2, "GTR", True),      # caterpillar: one node per level
     (6, 9, 100, 8, "HKY", False),     # many categories
     (7, 30, 130, 4, "GTR", False),    # chunks of 64+ classes per node, long segments
-    (8, 100, 30, 1, "GTR", False),    # many levels, one category
+    (8, 60, 30, 1, "GTR", False),     # many levels, one category
 ])
 def test_resident_random_trees(seed, S, P, C, model, cat):
     case = cases.random_case(seed, S=S, P=P, C=C, model=model, rooted=True, caterpillar=cat)
