@@ -1395,11 +1395,15 @@ __global__ void __launch_bounds__(256) finalize_kernel(FinArgs a) {
 //   rate (i,j): (f_j W_ij + f_i W_ji - f_j W_ii - f_i W_jj - 2 f_i f_j qw) / s
 //   freq m:     (sum_{j != m} R_jm (W_jm - W_jj) - qw sum_{j != m} 2 R_mj f_j) / s
 //               + the explicit root term.
-// One workgroup per draw; per-thread partial M over (c, b), then a
-// fixed-order sum: deterministic.  JC69 has no Q parameters: zeros.
-__global__ void __launch_bounds__(256) qgrad_kernel(FinArgs a) {
-  __shared__ double part[256][17];
-  const int draw = blockIdx.x, tid = threadIdx.x;
+// One workgroup per draw; per-thread partial M over (c, b) (the per-draw
+// V, V^-1, lambda and 1/(lambda_k - lambda_l) in LDS, so a thread holds only
+// M, G and one row of V^T G: ~100 VGPRs instead of 200, twice the resident
+// waves), a wave reduction of the 16 partials, then the waves in order:
+// deterministic.  JC69 has no Q parameters: zeros.
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) qgrad_kernel(FinArgs a) {
+  __shared__ double sV[16], sVi[16], srinv[16], slam[4];
+  __shared__ double part[4][16];
+  const int draw = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int C = a.C, B = a.B;
   double* out = a.out + (size_t)draw * a.outlen;
   const int o = 1 + B + 2 * C;
@@ -1408,88 +1412,95 @@ __global__ void __launch_bounds__(256) qgrad_kernel(FinArgs a) {
     return;
   }
   const double* e = a.eig + (size_t)draw * EIG_LEN;
-  double V[16], Vi[16], lam[4];
-#pragma unroll
-  for (int k = 0; k < 16; ++k) {
-    V[k] = e[EIG_M1 + k];
-    Vi[k] = e[EIG_M2 + k];
+  if (tid < 16) {
+    sV[tid] = e[EIG_M1 + tid];
+    sVi[tid] = e[EIG_M2 + tid];
+    // 1 / (lam_k - lam_l) once per draw (0 marks a tie: t e^{lam_k t} there)
+    const double lk = e[EIG_LAM + (tid >> 2)], ll = e[EIG_LAM + (tid & 3)];
+    const double d = lk - ll;
+    srinv[tid] = fabs(d) < 1e-12 * fmax(1.0, fabs(lk)) ? 0.0 : 1.0 / d;
+    if (tid < 4) slam[tid] = e[EIG_LAM + tid];
   }
-#pragma unroll
-  for (int k = 0; k < 4; ++k) lam[k] = e[EIG_LAM + k];
+  __syncthreads();
   const double* mdl = a.model + (size_t)draw * (10 + 2 * C);
   const double* bl = a.blens + (size_t)draw * B;
   const double* rows = a.grows + (size_t)draw * a.grows_stride;
-  // 1 / (lam_k - lam_l) once per draw (0 marks a tie: t e^{lam_k t} there)
-  double rinv[16];
-#pragma unroll
-  for (int k = 0; k < 4; ++k)
-#pragma unroll
-    for (int l = 0; l < 4; ++l) {
-      const double d = lam[k] - lam[l];
-      rinv[k * 4 + l] = fabs(d) < 1e-12 * fmax(1.0, fabs(lam[k])) ? 0.0 : 1.0 / d;
-    }
-  double m[16];
-#pragma unroll
-  for (int k = 0; k < 16; ++k) m[k] = 0.0;
-  for (int idx = tid; idx < C * B; idx += blockDim.x) {
+  // a quad of lanes per (c, b): lane k forms row k of H = V^T G V^-T and
+  // accumulates row k of M (4 values); e^{lam_k t} comes from lane k
+  const int k = tid & 3;
+  double m[4] = {0.0, 0.0, 0.0, 0.0};
+  for (int idx = tid >> 2; idx < C * B; idx += (int)(blockDim.x >> 2)) {
     const int c = idx / B, b = idx - c * B;
     const double t = mdl[10 + c] * bl[b];
     double G[16];
+    const double2* g2 = reinterpret_cast<const double2*>(rows + (size_t)idx * 16);
 #pragma unroll
-    for (int k = 0; k < 16; ++k) G[k] = rows[(size_t)idx * 16 + k];
-    double T[16];  // V^T G
-#pragma unroll
-    for (int k = 0; k < 4; ++k)
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        double acc = 0.0;
-#pragma unroll
-        for (int i = 0; i < 4; ++i) acc = fma(V[i * 4 + k], G[i * 4 + j], acc);
-        T[k * 4 + j] = acc;
-      }
+    for (int u = 0; u < 8; ++u) {
+      const double2 v = g2[u];
+      G[2 * u] = v.x;
+      G[2 * u + 1] = v.y;
+    }
+    const double Ek = exp(slam[k] * t);
     double E[4];
-#pragma unroll
-    for (int k = 0; k < 4; ++k) E[k] = exp(lam[k] * t);
-#pragma unroll
-    for (int k = 0; k < 4; ++k)
-#pragma unroll
-      for (int l = 0; l < 4; ++l) {
-        double h = 0.0;  // (V^T G V^-T)[k][l]
-#pragma unroll
-        for (int j = 0; j < 4; ++j) h = fma(T[k * 4 + j], Vi[l * 4 + j], h);
-        const double ri = rinv[k * 4 + l];
-        const double phi = ri == 0.0 ? t * E[k] : (E[k] - E[l]) * ri;
-        m[k * 4 + l] = fma(h, phi, m[k * 4 + l]);
-      }
-  }
-#pragma unroll
-  for (int k = 0; k < 16; ++k) part[tid][k] = m[k];
-  __syncthreads();
-  if (tid < 16) {
-    double acc = 0.0;
-    for (int q = 0; q < (int)blockDim.x; ++q) acc += part[q][tid];
-    part[0][tid] = acc;  // row 0 is read only by thread tid itself above
-  }
-  __syncthreads();
-  if (tid != 0) return;
-  double M[16], W[16];
-#pragma unroll
-  for (int k = 0; k < 16; ++k) M[k] = part[0][k];
-  // W = V^-T M V^T: W[i][j] = sum_kl Vi[k][i] M[k][l] V[j][l]
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
+    E[0] = dpp_d<0x00>(Ek);
+    E[1] = dpp_d<0x55>(Ek);
+    E[2] = dpp_d<0xAA>(Ek);
+    E[3] = dpp_d<0xFF>(Ek);
+    double T[4];  // row k of V^T G
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       double acc = 0.0;
 #pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        double ml = 0.0;
-#pragma unroll
-        for (int l = 0; l < 4; ++l) ml = fma(M[k * 4 + l], V[j * 4 + l], ml);
-        acc = fma(Vi[k * 4 + i], ml, acc);
-      }
-      W[i * 4 + j] = acc;
+      for (int i = 0; i < 4; ++i) acc = fma(sV[i * 4 + k], G[i * 4 + j], acc);
+      T[j] = acc;
     }
+#pragma unroll
+    for (int l = 0; l < 4; ++l) {
+      double h = 0.0;  // (V^T G V^-T)[k][l]
+#pragma unroll
+      for (int j = 0; j < 4; ++j) h = fma(T[j], sVi[l * 4 + j], h);
+      const double ri = srinv[k * 4 + l];
+      const double phi = ri == 0.0 ? t * Ek : (Ek - E[l]) * ri;
+      m[l] = fma(h, phi, m[l]);
+    }
+  }
+  // sum over the wave's 16 quads (lane bits 2..5): lanes with bits 2, 3 clear
+  // end with M[k][2 b5 + b4]
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    swap32(m[u], m[u + 2]);
+    m[u] += m[u + 2];
+  }
+  swap16(m[0], m[1]);
+  m[0] += m[1];
+  m[0] += dpp_d<DPP_ROW_ROR8>(m[0]);
+  m[0] += dpp_d<0x124>(m[0]);  // row_ror:4 (symmetric after the ror:8 stage)
+  if ((lane & 12) == 0) part[wave][k * 4 + ((lane >> 5) & 1) * 2 + ((lane >> 4) & 1)] = m[0];
+  __syncthreads();
+  // M = the waves' partials in order; W = V^-T M V^T, one entry per thread:
+  // W[i][j] = sum_kl Vi[k][i] M[k][l] V[j][l]
+  __shared__ double sM[16], sW[16];
+  const int nw = (int)(blockDim.x >> 6);
+  if (tid < 16) {
+    double acc = part[0][tid];
+    for (int w = 1; w < nw; ++w) acc += part[w][tid];
+    sM[tid] = acc;
+  }
+  __syncthreads();
+  if (tid < 16) {
+    const int i = tid >> 2, j = tid & 3;
+    double acc = 0.0;
+    for (int k = 0; k < 4; ++k) {
+      double ml = 0.0;
+      for (int l = 0; l < 4; ++l) ml = fma(sM[k * 4 + l], sV[j * 4 + l], ml);
+      acc = fma(sVi[k * 4 + i], ml, acc);
+    }
+    sW[tid] = acc;
+  }
+  __syncthreads();
+  if (tid != 0) return;
+  double W[16];
+  for (int k = 0; k < 16; ++k) W[k] = sW[k];
   const double* Q = e + EIG_Q;
   const double s = e[EIG_S];
   double qw = 0.0;
