@@ -1282,12 +1282,15 @@ __global__ void __launch_bounds__(256) gsum_kernel(FinArgs a) {
   }
 }
 
-// One workgroup per draw (dL/dP rows already in place: sweep or gsum).
+// One workgroup per draw (dL/dP rows already in place: sweep or gsum); 1024
+// threads when a draw has many scalar slots (launch_finalize), so the slot
+// sums are a few rounds of loads in flight instead of a long latency chain
+// (the synthetic workload's 2,063 root chunks: 38 us with 256 threads).
 //   scalars log L, dlogL/dps, root-frequency term: wave 0, lane-strided
 //           over slots + a fixed-shape wave reduction;
 //   chain rule  dlogL/dt_{b,c} = <G_bc, Q P_bc>,  dlogL/db = sum_c r_c (.),
 //           dlogL/dr_c = sum_b b (.)   (generate_script.py:663-671 blens).
-__global__ void __launch_bounds__(256) finalize_kernel(FinArgs a) {
+__global__ void __launch_bounds__(1024) finalize_kernel(FinArgs a) {
   extern __shared__ double fsh[];  // inner[C*B], Q[16]
   const int draw = blockIdx.x;
   const int C = a.C, B = a.B;
@@ -2004,6 +2007,8 @@ int timing_begin(phy_ctx* ctx, hipStream_t st, hipEvent_t* e0, hipEvent_t* e1) {
   return PHY_OK;
 }
 
+void launch_finalize(const FinArgs& fa, int n, hipStream_t st);
+
 // The class sweep (class_engine.inc): forward levels, root, reverse levels,
 // then the ordered dL/dP sums and the shared finalize.  The timed region
 // (phy_timing_*) spans the forward through the last reverse level.
@@ -2073,13 +2078,19 @@ int launch_class(phy_ctx* ctx, int n, const double* d_blens, const double* d_mod
   FinArgs fa{ctx->d_gslot, e->d_sslot, ctx->d_pmat, ctx->d_eig, d_blens, d_model, ctx->d_gpos, ctx->d_inner, d_out,
              C,            B,          ctx->nmat,   e->nrootch,  phy_output_len(ctx), 0, ctx->R, grows, gstride,
              ctx->kind};
-  hipLaunchKernelGGL(finalize_kernel, dim3(n), dim3(256), ((size_t)C * B + 16 + 256) * sizeof(double), st, fa);
+  launch_finalize(fa, n, st);
   HIP_TRY(hipGetLastError());
   return PHY_OK;
 }
 
 int launch_pattern(phy_ctx* ctx, int n, const double* d_blens, const double* d_model, double* d_out,
                    double* d_site, hipStream_t st, double* grows, long long gstride);
+
+void launch_finalize(const FinArgs& fa, int n, hipStream_t st) {
+  const int threads = fa.gx > 64 ? 1024 : 256;
+  hipLaunchKernelGGL(finalize_kernel, dim3(n), dim3(threads), ((size_t)fa.C * fa.B + 16 + threads) * sizeof(double),
+                     st, fa);
+}
 
 // The resident class sweep (resident_engine.inc): forward + root L, then the
 // forward again with the reverse, one workgroup per (draw, category) each
@@ -2105,7 +2116,7 @@ int launch_res(phy_ctx* ctx, int n, const double* d_blens, const double* d_model
   FinArgs fa{ctx->d_gslot, e->d_sslot, ctx->d_pmat, ctx->d_eig, d_blens, d_model, ctx->d_gpos, ctx->d_inner, d_out,
              C,            B,          ctx->nmat,   1,           phy_output_len(ctx), 0, ctx->R, grows, gstride,
              ctx->kind};
-  hipLaunchKernelGGL(finalize_kernel, dim3(n), dim3(256), ((size_t)C * B + 16 + 256) * sizeof(double), st, fa);
+  launch_finalize(fa, n, st);
   HIP_TRY(hipGetLastError());
   return PHY_OK;
 }
@@ -2180,7 +2191,7 @@ int launch_pattern(phy_ctx* ctx, int n, const double* d_blens, const double* d_m
     HIP_TRY(hipGetLastError());
   }
   if (!fin) {
-    hipLaunchKernelGGL(finalize_kernel, dim3(n), dim3(256), ((size_t)C * B + 16 + 256) * sizeof(double), st, fa);
+    launch_finalize(fa, n, st);
     HIP_TRY(hipGetLastError());
   }
   return PHY_OK;
