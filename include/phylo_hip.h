@@ -180,11 +180,15 @@ int phy_set_output(phy_ctx* ctx, int compact);
  * (site repeats: the forward pass once per distinct tip-state tuple of each
  * subtree, the reverse on upper partials aggregated per tuple -- the exact,
  * total form of the reference's column-reuse cache, pruner/tree.cpp:140-174),
+ * 3 = resident class sweep (the class sweep with each (draw, category)'s
+ * whole class state in LDS, one workgroup per (draw, category); rooted trees
+ * whose state fits in 160 KiB only, else PHY_EINVAL; measured slower than
+ * the pattern sweep on fluA / HCV, so never chosen automatically),
  * 0 = automatic (class sweep for alignments of >= 16384 patterns whose
  * subtree classes are at most a quarter of the pattern sweep's node-pattern
  * work).  Results agree to rounding either way.  PHY_ENGINE sets the default
  * at phy_create.  phy_engine returns the engine the next launch uses (0
- * pattern, 1 class). */
+ * pattern, 1 class, 2 resident). */
 int phy_set_engine(phy_ctx* ctx, int mode);
 int phy_engine(const phy_ctx* ctx);
 
