@@ -454,7 +454,7 @@ def main():
     achieved = alg / (kern_avg_ms * 1e-3) / 1e9
     traffic = None
     pmc = os.path.join(ROOT, "profiles", "pmc_traffic.json")
-    if os.path.exists(pmc):
+    if os.path.exists(pmc) and args.shard_of <= 1:  # the PMC record is of the whole workload, not a shard
         try:
             with open(pmc) as fp:
                 rec = json.load(fp)
