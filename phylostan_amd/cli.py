@@ -200,6 +200,8 @@ def run(arg, likelihood_factory=None, log=print):
         from .engine import TreeLikelihood
         dev = arg.device if arg.device is not None else int(os.environ.get("LOCAL_RANK", "0"))
         lik = TreeLikelihood(d.tipcodes, d.weights, d.peel0, d.rooted, arg.model, C, max_draws=max_draws, device=dev)
+        if max_draws * C <= 256:  # batches within one workgroup per CU: the lowest-latency engine
+            lik.prefer_latency_engine()
     else:
         lik = likelihood_factory(d.tipcodes, d.weights, d.peel0, d.rooted, arg.model, C)
     tree = TreeData.from_phylodata(d)

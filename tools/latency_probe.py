@@ -19,6 +19,7 @@ def main():
     ap.add_argument("--draws", type=int, default=4)
     ap.add_argument("--calls", type=int, default=300)
     ap.add_argument("--workload", default="fluA", choices=["fluA", "HCV", "DS1"])
+    ap.add_argument("--engine", default="auto", choices=["auto", "pattern", "class", "resident"])
     a = ap.parse_args()
     from phylostan_amd.engine import TreeLikelihood
     from tests import cases
@@ -26,6 +27,8 @@ def main():
     lik = TreeLikelihood(case.tipcodes, case.weights, case.peel0, case.rooted, case.model, case.C,
                          max_draws=a.draws)
     lik.set_output(compact=True)
+    if a.engine != "auto":
+        lik.set_engine(a.engine)
     bl = np.stack([case.blens * (1.0 + 0.01 * k) for k in range(a.draws)])
     mv = np.stack([case.model_vec()] * a.draws)
     for _ in range(20):
@@ -34,7 +37,7 @@ def main():
     for _ in range(a.calls):
         lik.evaluate_batch(bl, mv)
     dt = (time.perf_counter() - t0) / a.calls
-    print(json.dumps({"workload": a.workload, "draws": a.draws, "us_per_call": dt * 1e6}))
+    print(json.dumps({"workload": a.workload, "engine": lik.engine(), "draws": a.draws, "us_per_call": dt * 1e6}))
 
 
 if __name__ == "__main__":

@@ -28,6 +28,8 @@ def main():
     ap.add_argument("--warmup", type=int, default=1000)
     ap.add_argument("--samples", type=int, default=1000)
     ap.add_argument("--seed", type=int, default=1)
+    ap.add_argument("--engine", default="latency", choices=["latency", "auto", "pattern", "resident"],
+                    help="latency: the resident class sweep when it applies (what the CLI uses for NUTS)")
     ap.add_argument("--out", default=os.path.join(ROOT, "gpurun_out", "config5"))
     a = ap.parse_args()
     os.makedirs(a.out, exist_ok=True)
@@ -44,6 +46,10 @@ def main():
     spec = ModelSpec(model="HKY", categories=4, clock="strict", estimate_rate=True, coalescent="constant",
                      heterochronous=True)
     lik = TreeLikelihood(d["tipbits"], d["weights"], peel0, True, "HKY", 4, max_draws=a.chains)
+    if a.engine == "latency":
+        lik.prefer_latency_engine()
+    elif a.engine != "auto":
+        lik.set_engine(a.engine)
     post = Posterior(spec, tree, lik)
     q0s = [post.initial_point(np.random.default_rng((a.seed, c))) for c in range(a.chains)]
     t0 = time.time()
@@ -72,6 +78,7 @@ def main():
     n_grad = sum(ch.n_grad for ch in chains)
     rec = {"config": "fluA HKY+W4 strict clock, constant coalescent, NUTS %d chains x (%d warmup + %d draws)"
                      % (a.chains, a.warmup, a.samples),
+           "engine": lik.engine(),
            "wall_s": el, "gradient_evaluations": n_grad, "grads_per_s": n_grad / el,
            "divergent": int(sum(dr[6] for ch in chains for dr in ch.draws if not dr[8])),
            "mean_accept": float(np.mean([dr[2] for ch in chains for dr in ch.draws if not dr[8]])),
