@@ -117,6 +117,19 @@ int phy_eval(phy_ctx* ctx, int n_draws, const double* blens, const double* model
 int phy_eval_device(phy_ctx* ctx, int n_draws, const double* d_blens, const double* d_model,
                     double* d_out, double* d_site_ll, void* stream);
 
+/* Asynchronous small batches (host buffers, 1 <= n_draws <= min(max_draws,
+ * 64)): phy_eval_submit copies the inputs into the context's pinned staging
+ * and queues the upload, the evaluation and the download of the output rows
+ * on the context's stream, then returns; phy_eval_wait blocks until they are
+ * done and copies the n_draws rows (phy_output_len doubles each) into `out`.
+ * One submission in flight per context (phy_eval refuses while one is);
+ * contexts on one device run concurrently, so a sampler can overlap one
+ * group of chains' host work with another group's evaluation.  phy_eval is
+ * submit + wait (plus site log-likelihoods).  No reference counterpart: the
+ * reference's log_prob is synchronous (eigen/prune_stan.hpp:9-17). */
+int phy_eval_submit(phy_ctx* ctx, int n_draws, const double* blens, const double* model);
+int phy_eval_wait(phy_ctx* ctx, double* out);
+
 /* Mirror of the reference's external Stan function: the double overload
  * returns log P (eigen/eigen.j2:171-177); with grad != NULL it also fills
  * dlogL/dblens[B] -- the `grads` that prune_stan.hpp:16 hands to

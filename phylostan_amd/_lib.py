@@ -31,6 +31,8 @@ SIGNATURES = {
     "phy_program_info": (ctypes.c_int, [ctypes.c_void_p, _c_int_p, _c_int_p, _c_int_p, _c_int_p]),
     "phy_eval": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p,
                                 ctypes.c_void_p, ctypes.c_void_p]),
+    "phy_eval_submit": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p]),
+    "phy_eval_wait": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p]),
     "phy_eval_device": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p,
                                        ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
     "phy_pruning_loglik": (ctypes.c_double, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,

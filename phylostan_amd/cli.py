@@ -199,10 +199,16 @@ def run(arg, likelihood_factory=None, log=print):
     if likelihood_factory is None:
         from .engine import TreeLikelihood
         dev = arg.device if arg.device is not None else int(os.environ.get("LOCAL_RANK", "0"))
-        lik = TreeLikelihood(d.tipcodes, d.weights, d.peel0, d.rooted, arg.model, C, max_draws=max_draws, device=dev)
-        if max_draws * C <= 256:  # batches within one workgroup per CU: the lowest-latency engine
-            lik.prefer_latency_engine()
+
+        def make_lik():
+            lk = TreeLikelihood(d.tipcodes, d.weights, d.peel0, d.rooted, arg.model, C, max_draws=max_draws,
+                                device=dev)
+            if max_draws * C <= 256:  # batches within one workgroup per CU: the lowest-latency engine
+                lk.prefer_latency_engine()
+            return lk
+        lik = make_lik()
     else:
+        make_lik = None
         lik = likelihood_factory(d.tipcodes, d.weights, d.peel0, d.rooted, arg.model, C)
     tree = TreeData.from_phylodata(d)
     if not spec.heterochronous:
@@ -244,7 +250,10 @@ def run(arg, likelihood_factory=None, log=print):
     num_samples = arg.iter - num_warmup
     q0s = [post.initialize(np.random.default_rng((seed, c, 0))) for c in range(chains)]
     t0 = time.time()
-    res = run_chains(post, q0s, [(seed, c) for c in range(chains)], num_warmup=num_warmup,
+    # two groups of chains on two contexts, pipelined: one group's host work
+    # overlaps the other's GPU evaluation (nuts.run_chains)
+    posts = [post, Posterior(spec, tree, make_lik())] if make_lik is not None and chains >= 2 else post
+    res = run_chains(posts, q0s, [(seed, c) for c in range(chains)], num_warmup=num_warmup,
                      num_samples=num_samples, thin=arg.thin, progress=log, algorithm=arg.algorithm)
     el = time.time() - t0
     for c, ch in enumerate(res):

@@ -1595,6 +1595,7 @@ struct phy_ctx {
   double* h_in = nullptr;   // pinned [PIN_DRAWS][B + model_len]
   double* h_out = nullptr;  // pinned [PIN_DRAWS][full output row]
   double* d_in = nullptr;   // device [PIN_DRAWS][B + model_len]
+  int pending = 0;          // draws of a phy_eval_submit not yet collected by phy_eval_wait
   double2* d_scratch = nullptr;
   double2* d_dstk = nullptr;
   double* d_gslot = nullptr;
@@ -2459,9 +2460,46 @@ int phy_eval_device(phy_ctx* ctx, int n_draws, const double* d_blens, const doub
   return launch(ctx, n_draws, d_blens, d_model, d_out, d_site_ll, st);
 }
 
+// phy_eval_submit / phy_eval_wait: the small-batch path split at the stream
+// synchronisation, so a host can overlap its own work (or another context's
+// GPU work) with this evaluation.
+int phy_eval_submit(phy_ctx* ctx, int n_draws, const double* blens, const double* model) {
+  if (!ctx) return fail(PHY_EINVAL, "NULL ctx");
+  if (ctx->pending) return fail(PHY_EINVAL, "phy_eval_submit: an evaluation is already in flight");
+  if (n_draws < 1 || n_draws > ctx->max_draws || n_draws > PIN_DRAWS || !ctx->h_in || !ctx->h_out || !ctx->d_in)
+    return fail(PHY_ERANGE, "phy_eval_submit: n_draws must be in [1, min(max_draws, 64)]");
+  if (!blens || !model) return fail(PHY_EINVAL, "NULL host buffer");
+  HIP_TRY(hipSetDevice(ctx->device));
+  hipStream_t st = ctx->stream;
+  const int ml = 10 + 2 * ctx->C;
+  const size_t nb = (size_t)n_draws * ctx->B, nm = (size_t)n_draws * ml;
+  const size_t no = (size_t)n_draws * phy_output_len(ctx);
+  std::memcpy(ctx->h_in, blens, sizeof(double) * nb);
+  std::memcpy(ctx->h_in + nb, model, sizeof(double) * nm);
+  HIP_TRY(hipMemcpyAsync(ctx->d_in, ctx->h_in, sizeof(double) * (nb + nm), hipMemcpyHostToDevice, st));
+  int rc = launch(ctx, n_draws, ctx->d_in, ctx->d_in + nb, ctx->d_out, nullptr, st);
+  if (rc) return rc;
+  HIP_TRY(hipMemcpyAsync(ctx->h_out, ctx->d_out, sizeof(double) * no, hipMemcpyDeviceToHost, st));
+  ctx->pending = n_draws;
+  return PHY_OK;
+}
+
+int phy_eval_wait(phy_ctx* ctx, double* out) {
+  if (!ctx) return fail(PHY_EINVAL, "NULL ctx");
+  if (!ctx->pending) return fail(PHY_EINVAL, "phy_eval_wait: nothing submitted");
+  if (!out) return fail(PHY_EINVAL, "NULL host buffer");
+  HIP_TRY(hipSetDevice(ctx->device));
+  const int n = ctx->pending;
+  ctx->pending = 0;
+  HIP_TRY(hipStreamSynchronize(ctx->stream));
+  std::memcpy(out, ctx->h_out, sizeof(double) * (size_t)n * phy_output_len(ctx));
+  return PHY_OK;
+}
+
 int phy_eval(phy_ctx* ctx, int n_draws, const double* blens, const double* model, double* out,
              double* site_ll) {
   if (!ctx) return fail(PHY_EINVAL, "NULL ctx");
+  if (ctx->pending) return fail(PHY_EINVAL, "phy_eval: a phy_eval_submit is still in flight (phy_eval_wait first)");
   if (n_draws < 1 || n_draws > ctx->max_draws) return fail(PHY_ERANGE, "n_draws out of range");
   if (!blens || !model || !out) return fail(PHY_EINVAL, "NULL host buffer");
   HIP_TRY(hipSetDevice(ctx->device));

@@ -66,6 +66,8 @@ class TreeLikelihood:
     device   : HIP device ordinal
     """
 
+    _pending = 0  # draws of a submit_rows not yet collected
+
     def __init__(self, tipcodes, weights, peel0, rooted, model, C, max_draws=1, device=0):
         self.lib = _lib.load()
         tipcodes = np.ascontiguousarray(tipcodes, dtype=np.uint8)
@@ -142,6 +144,24 @@ class TreeLikelihood:
         out = np.empty((n, self.outlen))
         _lib.check(self.lib.phy_eval(self.ctx, n, blens.ctypes.data, mv.ctypes.data, out.ctypes.data, None),
                    "phy_eval")
+        return out
+
+    def submit_rows(self, blens, model_vecs):
+        """Start an evaluation of n <= 64 draws (phy_eval_submit) and return
+        at once; ``wait_rows`` collects its raw output rows."""
+        blens = np.ascontiguousarray(np.atleast_2d(blens), dtype=np.float64)
+        mv = np.ascontiguousarray(np.atleast_2d(model_vecs), dtype=np.float64)
+        n = blens.shape[0]
+        if blens.shape != (n, self.B) or mv.shape != (n, self.model_len):
+            raise ValueError("bad shapes: blens %s model %s" % (blens.shape, mv.shape))
+        _lib.check(self.lib.phy_eval_submit(self.ctx, n, blens.ctypes.data, mv.ctypes.data), "phy_eval_submit")
+        self._pending = n
+
+    def wait_rows(self):
+        """The rows [n, outlen] of the evaluation ``submit_rows`` started."""
+        out = np.empty((self._pending, self.outlen))
+        self._pending = 0
+        _lib.check(self.lib.phy_eval_wait(self.ctx, out.ctypes.data), "phy_eval_wait")
         return out
 
     def evaluate(self, blens, model_vec, site_ll=False):

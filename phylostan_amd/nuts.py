@@ -369,30 +369,60 @@ def run_chains(posterior, q0s, seeds, num_warmup=1000, num_samples=1000, thin=1,
                max_depth=10, algorithm="nuts", **kw):
     """Run ``len(q0s)`` NUTS (or static HMC) chains in lockstep, batching
     every round of gradient requests into one ``posterior.log_prob_grad``
-    call."""
+    call.
+
+    ``posterior`` may be a list of posteriors (the same model on separate
+    likelihood contexts): chain i then belongs to group i mod len(list), and
+    the groups are pipelined -- while one group's likelihood evaluates on the
+    GPU (``log_prob_grad_begin`` / ``_end``), the host finishes and advances
+    the other groups.  Every chain sees exactly the values it would see
+    alone: evaluations are per draw, independent of the batch."""
+    posts = list(posterior) if isinstance(posterior, (list, tuple)) else [posterior]
+    dim = posts[0].dim
     if algorithm == "hmc":
-        chains = [StaticHMCChain(posterior.dim, q0, np.random.default_rng(sd), num_warmup, num_samples, thin, **kw)
+        chains = [StaticHMCChain(dim, q0, np.random.default_rng(sd), num_warmup, num_samples, thin, **kw)
                   for q0, sd in zip(q0s, seeds)]
     else:
-        chains = [Chain(posterior.dim, q0, np.random.default_rng(sd), num_warmup, num_samples, thin,
+        chains = [Chain(dim, q0, np.random.default_rng(sd), num_warmup, num_samples, thin,
                         max_depth=max_depth, **kw) for q0, sd in zip(q0s, seeds)]
     gens = [c.program() for c in chains]
     pending = {}
     for i, g in enumerate(gens):
         pending[i] = next(g)
+    ng = len(posts)
+    groups = [[i for i in range(len(chains)) if i % ng == k] for k in range(ng)]
     rounds = 0
     t0 = time.time()
-    while pending:
-        idx = sorted(pending)
+
+    def submit(k):
+        idx = [i for i in groups[k] if i in pending]
+        if not idx:
+            return None
         Q = np.stack([pending[i] for i in idx])
-        lp, G = posterior.log_prob_grad(Q)
-        for k, i in enumerate(idx):
-            try:
-                pending[i] = gens[i].send((float(lp[k]), G[k]))
-            except StopIteration:
-                del pending[i]
-        rounds += 1
-        if progress and rounds % 2000 == 0:
-            progress("%s: %d batched gradient rounds, %d draws (chain 0), %.1f s"
-                     % (algorithm.upper(), rounds, len(chains[0].draws), time.time() - t0))
+        if hasattr(posts[k], "log_prob_grad_begin"):
+            return idx, posts[k].log_prob_grad_begin(Q)
+        return idx, Q  # a plain log_prob_grad posterior: evaluated in finish
+
+    def finish(k, tok):
+        if hasattr(posts[k], "log_prob_grad_end"):
+            return posts[k].log_prob_grad_end(tok)
+        return posts[k].log_prob_grad(tok)
+
+    tokens = [submit(k) for k in range(ng)]
+    while any(t is not None for t in tokens):
+        for k in range(ng):
+            if tokens[k] is None:
+                continue
+            idx, tok = tokens[k]
+            lp, G = finish(k, tok)
+            for j, i in enumerate(idx):
+                try:
+                    pending[i] = gens[i].send((float(lp[j]), G[j]))
+                except StopIteration:
+                    del pending[i]
+            tokens[k] = submit(k)
+            rounds += 1
+            if progress and rounds % (2000 * ng) == 0:
+                progress("%s: %d gradient rounds, %d draws (chain 0), %.1f s"
+                         % (algorithm.upper(), rounds, len(chains[0].draws), time.time() - t0))
     return chains

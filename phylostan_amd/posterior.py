@@ -351,11 +351,11 @@ class Posterior:
             return rs, ps
         return np.ones((n, 1)), np.ones((n, 1))
 
-    def _lik_rows(self, blens, mv, width):
-        """The likelihood's compact output rows [n, width] (the engine's raw
-        rows when it offers them, else assembled from EvalResult objects)."""
+    def _lik_rows(self, blens, mv):
+        """The likelihood's output rows [n, >= 1 + B + 2C + 14] (the engine's
+        raw rows when it offers them, else assembled from EvalResult objects)."""
         if hasattr(self.lik, "evaluate_rows"):
-            return self.lik.evaluate_rows(blens, mv)[:, :width]
+            return self.lik.evaluate_rows(blens, mv)
         return np.stack([np.concatenate([[r.loglik], r.grad_blens, r.grad_rs, r.grad_ps, r.grad_freq_root,
                                          r.grad_rates, r.grad_freqs]) for r in self.lik.evaluate_batch(blens, mv)])
 
@@ -483,24 +483,69 @@ class Posterior:
         -inf, zero gradient, and neither the transforms' numpy nor the GPU
         sees them.  Draws in support whose arithmetic still overflows are
         rejected the same way after evaluation."""
+        return self.log_prob_grad_end(self.log_prob_grad_begin(U, propto, need_grad))
+
+    def log_prob_grad_begin(self, U, propto=True, need_grad=True):
+        """First half of ``log_prob_grad``: the host work up to the likelihood,
+        whose evaluation is started (asynchronously when the engine offers
+        ``submit_rows``); ``log_prob_grad_end`` finishes.  Lets a sampler
+        overlap one group of chains' host work with another's GPU work."""
         U = np.atleast_2d(np.asarray(U, np.float64))
         n = U.shape[0]
         with np.errstate(all="ignore"):
             ok, vals, states, logj = self._support(U, *self.constrain(np.where(np.isfinite(U), U, 0.0)))
+        tok = {"n": n, "ok": ok, "need_grad": need_grad, "gen": None}
+        if ok.any():
+            pre = (vals, states, logj) if ok.all() else None  # the usual case: the constrained values are reused
+            gen = self._lpg_gen(U[ok], propto, need_grad, pre)
+            try:
+                with np.errstate(all="ignore"):
+                    req = next(gen)
+            except StopIteration as e:
+                tok["done"] = e.value
+                return tok
+            tok["gen"] = gen
+            if hasattr(self.lik, "submit_rows") and req[0].shape[0] <= 64:
+                self.lik.submit_rows(*req)
+                tok["async"] = True
+            else:
+                with np.errstate(all="ignore"):
+                    tok["rows"] = self._lik_rows(*req)
+        return tok
+
+    def log_prob_grad_end(self, tok):
+        n, ok, need_grad = tok["n"], tok["ok"], tok["need_grad"]
         lp = np.full(n, -np.inf)
         G = np.zeros((n, self.dim)) if need_grad else None
-        if ok.any():
-            pre = None
-            if ok.all():  # the usual case: the constrained values are reused
-                pre = (vals, states, logj)
-            with np.errstate(all="ignore"):
-                lp_ok, g_ok = self._log_prob_grad_rows(U[ok], propto, need_grad, pre)
-            lp[ok] = lp_ok
+        res = tok.get("done")
+        if tok["gen"] is not None:
+            rows = self.lik.wait_rows() if tok.get("async") else tok["rows"]
+            try:
+                with np.errstate(all="ignore"):
+                    tok["gen"].send(rows)
+                raise RuntimeError("internal: log-density generator did not finish")
+            except StopIteration as e:
+                res = e.value
+        if res is not None:
+            lp[ok] = res[0]
             if need_grad:
-                G[ok] = g_ok
+                G[ok] = res[1]
         return lp, G
 
     def _log_prob_grad_rows(self, U, propto=True, need_grad=True, pre=None):
+        """The in-support rows' (lp, grad), evaluating the likelihood at once."""
+        gen = self._lpg_gen(U, propto, need_grad, pre)
+        try:
+            req = next(gen)
+            gen.send(self._lik_rows(*req))
+        except StopIteration as e:
+            return e.value
+        raise RuntimeError("internal: log-density generator did not finish")
+
+    def _lpg_gen(self, U, propto=True, need_grad=True, pre=None):
+        """Generator: yields the likelihood request (blens [m, B], model
+        vectors [m, 10 + 2C]) of the draws that reach it, receives their output
+        rows, returns (lp, grad) through StopIteration."""
         n = U.shape[0]
         sp = self.spec
         S, C = self.S, self.C
@@ -533,7 +578,8 @@ class Posterior:
         rows[:, 0] = -np.inf
         if ok.any():
             sel = np.nonzero(ok)[0]
-            rows[sel] = self._lik_rows(blens[sel], mv[sel], o + 14)
+            got = yield (blens[sel], mv[sel])
+            rows[sel] = got[:, :o + 14]
         ll = rows[:, 0]
         lp = lp + ll
         bad = ~np.isfinite(lp)
