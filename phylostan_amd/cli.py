@@ -250,10 +250,10 @@ def run(arg, likelihood_factory=None, log=print):
     num_samples = arg.iter - num_warmup
     q0s = [post.initialize(np.random.default_rng((seed, c, 0))) for c in range(chains)]
     t0 = time.time()
-    # two groups of chains on two contexts, pipelined: one group's host work
-    # overlaps the other's GPU evaluation (nuts.run_chains)
-    posts = [post, Posterior(spec, tree, make_lik())] if make_lik is not None and chains >= 2 else post
-    res = run_chains(posts, q0s, [(seed, c) for c in range(chains)], num_warmup=num_warmup,
+    # one batched context for all chains: pipelining two chain groups on two
+    # contexts (run_chains with a list of posteriors) measured slower here --
+    # the host's per-call cost doubles
+    res = run_chains(post, q0s, [(seed, c) for c in range(chains)], num_warmup=num_warmup,
                      num_samples=num_samples, thin=arg.thin, progress=log, algorithm=arg.algorithm)
     el = time.time() - t0
     for c, ch in enumerate(res):

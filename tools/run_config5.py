@@ -28,7 +28,8 @@ def main():
     ap.add_argument("--warmup", type=int, default=1000)
     ap.add_argument("--samples", type=int, default=1000)
     ap.add_argument("--seed", type=int, default=1)
-    ap.add_argument("--groups", type=int, default=2, help="chain groups on separate contexts, pipelined")
+    ap.add_argument("--groups", type=int, default=1,
+                    help="chain groups on separate contexts, pipelined (2 measured slower: DESIGN.md 7)")
     ap.add_argument("--engine", default="latency", choices=["latency", "auto", "pattern", "resident"],
                     help="latency: the resident class sweep when it applies (what the CLI uses for NUTS)")
     ap.add_argument("--out", default=os.path.join(ROOT, "gpurun_out", "config5"))
