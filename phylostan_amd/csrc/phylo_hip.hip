@@ -2455,6 +2455,8 @@ int phy_eval_device(phy_ctx* ctx, int n_draws, const double* d_blens, const doub
   if (!ctx) return fail(PHY_EINVAL, "NULL ctx");
   if (n_draws < 1 || n_draws > ctx->max_draws) return fail(PHY_ERANGE, "n_draws out of range");
   if (!d_blens || !d_model || !d_out) return fail(PHY_EINVAL, "NULL device buffer");
+  if (ctx->pending)  // the submitted evaluation still uses the context's work buffers
+    return fail(PHY_EINVAL, "phy_eval_device: a phy_eval_submit is still in flight (phy_eval_wait first)");
   HIP_TRY(hipSetDevice(ctx->device));
   hipStream_t st = stream ? reinterpret_cast<hipStream_t>(stream) : ctx->stream;
   return launch(ctx, n_draws, d_blens, d_model, d_out, d_site_ll, st);

@@ -224,6 +224,28 @@ def test_nonfinite_is_minus_inf():
     assert res.loglik == -np.inf
 
 
+def test_submit_wait_equals_eval_and_guards_in_flight():
+    """phy_eval_submit / phy_eval_wait give phy_eval's rows bit for bit; a
+    second submit, phy_eval or phy_eval_device while one is in flight, and a
+    wait with nothing submitted are refused."""
+    from phylostan_amd._lib import PhyloHipError
+    case = cases.hcv_case()
+    eng = _engine(case, max_draws=4)
+    rng = np.random.default_rng(12)
+    bl = case.blens[None, :] * rng.uniform(0.8, 1.2, (3, 1))
+    mv = np.repeat(case.model_vec()[None], 3, axis=0)
+    ref = eng.evaluate_rows(bl, mv)
+    eng.submit_rows(bl, mv)
+    with pytest.raises(PhyloHipError):
+        eng.submit_rows(bl, mv)
+    with pytest.raises(PhyloHipError):
+        eng.evaluate_rows(bl, mv)
+    got = eng.wait_rows()
+    assert np.array_equal(got, ref)
+    with pytest.raises(PhyloHipError):
+        eng.wait_rows()
+
+
 def test_errors_are_loud():
     from phylostan_amd._lib import PhyloHipError
     case = cases.random_case(5, S=6, P=10, C=1, model="JC69")
