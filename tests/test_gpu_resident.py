@@ -116,3 +116,24 @@ def test_resident_refuses_unrooted():
     eng = _engine(case)
     with pytest.raises(_lib.PhyloHipError):
         eng.set_engine("resident")
+
+
+@pytest.mark.parametrize("block", range(4))
+def test_resident_fuzz_small_rooted(block):
+    """24 random rooted trees (3..48 taxa, 1..160 patterns, C 1..6, JC69 /
+    HKY / GTR, 10-40 % ambiguous tips, some caterpillars) against the oracle."""
+    rng = np.random.default_rng(500 + block)
+    for k in range(6):
+        S = int(rng.integers(3, 49))
+        P = int(rng.integers(1, 161))
+        C = int(rng.integers(1, 7))
+        model = ("JC69", "HKY", "GTR")[int(rng.integers(0, 3))]
+        case = cases.random_case(1000 * block + k, S=S, P=P, C=C, model=model, rooted=True,
+                                 caterpillar=bool(rng.random() < 0.3), ambiguous=float(rng.uniform(0.1, 0.4)))
+        eng = _engine(case)
+        try:
+            eng.set_engine("resident")
+        except _lib.PhyloHipError:  # class state beyond LDS: the refusal is the contract
+            assert eng.resident_info()["lds_bytes"] == 0
+            continue
+        check_case(case, eng)
