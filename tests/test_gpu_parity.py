@@ -180,6 +180,44 @@ def test_batched_draws_match_single(wg_budget):
         check_case(c, eng, res[k])
 
 
+@pytest.mark.parametrize("make,engine", [(cases.fluA_case, "pattern"), (cases.hcv_case, "pattern"),
+                                         (cases.fluA_case, "resident"), (cases.hcv_case, "class")],
+                         ids=["fluA-pattern", "HCV-pattern", "fluA-resident", "HCV-class"])
+def test_production_batch_every_row_vs_c_port(make, engine):
+    """The bench's shape: 1,024 distinct parameter draws in ONE launch (the
+    pattern sweep then runs one workgroup per draw with the finalize fused),
+    every output row -- log L, branch / rate / mixture / root-frequency
+    gradients, the device chain rule's exchangeability and frequency
+    gradients, dL/dP -- against the C port at the parity bar."""
+    from oracle import cpu
+    from phylostan_amd import models
+    base = make()
+    n = 1024
+    eng = _engine(base, max_draws=n)
+    eng.set_engine(engine)
+    rng = np.random.default_rng(17)
+    blens = base.blens[None, :] * rng.uniform(0.5, 1.5, (n, base.blens.size))
+    mvs = []
+    for k in range(n):
+        f = rng.dirichlet([30.0] * 4)
+        r = (models.hky_exchangeabilities(rng.uniform(2.0, 9.0)) if base.model == "HKY"
+             else base.rates * rng.uniform(0.7, 1.3, 6))
+        rs, ps = models.weibull_site_rates(rng.uniform(0.2, 2.0), base.C)
+        mvs.append(models.model_vector(f, r, rs, ps))
+    mvs = np.array(mvs)
+    rows = eng.evaluate_rows(blens, mvs)
+    kind = {"JC69": 0, "HKY": 1, "GTR": 2}[base.model]
+    for k in range(0, n, 37):  # 28 draws spread over the batch
+        ref, _ = cpu.evaluate(base.tipcodes, base.weights, base.peel0, True, kind, mvs[k], blens[k], base.C)
+        got = rows[k]
+        assert abs(got[0] - ref[0]) <= RTOL_LL * abs(ref[0])
+        B, C = eng.B, base.C
+        o = 1 + B + 2 * C
+        _close(got[1:o + 4], ref[1:o + 4], RTOL_G, "draw %d gradients" % k)
+        _close(got[o + 4:o + 14], ref[o + 4:o + 14], 1e-8, "draw %d Q-parameter gradients" % k)
+        _close(got[o + 14:], ref[o + 14:], RTOL_G, "draw %d dL/dP" % k)
+
+
 @pytest.mark.parametrize("lds_budget", [0, 30000])
 def test_persistent_workgroups_loop(lds_budget):
     """Fewer workgroups than pattern blocks: every workgroup loops (with the
