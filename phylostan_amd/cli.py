@@ -195,7 +195,8 @@ def run(arg, likelihood_factory=None, log=print):
     log("Model: " + arg.model)
     C = spec.C
     chains = max(1, arg.chains) if arg.algorithm in ("nuts", "hmc") else 1
-    max_draws = max(arg.elbo_samples, arg.grad_samples, chains, 1)
+    # draws per likelihood call: one per chain (NUTS / HMC), else the ELBO / gradient samples
+    max_draws = chains if arg.algorithm in ("nuts", "hmc") else max(arg.elbo_samples, arg.grad_samples, 1)
     if likelihood_factory is None:
         from .engine import TreeLikelihood
         dev = arg.device if arg.device is not None else int(os.environ.get("LOCAL_RANK", "0"))
