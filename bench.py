@@ -48,6 +48,8 @@ def parse():
     ap.add_argument("--sites", type=int, default=1_000_000, help="synthetic: simulated sites")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="cpu_baseline sample length")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-sampler-latency", action="store_true",
+                    help="skip the small-batch (sampler path) latency probe of the batched workloads")
     ap.add_argument("--single-eval", action="store_true",
                     help="also time unbatched (draws=1) evaluations and report them")
     ap.add_argument("--wg-budget", type=int, default=0)
@@ -441,6 +443,33 @@ def main():
         tb = time.perf_counter()
         single = dict(evals_per_s=n1 / (tb - ta), us_per_eval=1e6 * (tb - ta) / n1)
 
+    # the sampler path (host buffers, 4 draws per call, compact rows): µs per
+    # call on the pattern sweep and on the resident class sweep, which the
+    # CLI's NUTS / HMC / ADVI contexts use when it applies
+    sampler = None
+    if batched and rank == 0 and world == 1 and not args.no_sampler_latency:
+        from phylostan_amd.engine import TreeLikelihood
+        sampler = {"draws_per_call": 4}
+        bl4 = blens[0][:4].copy()
+        mv4 = mvs[0][:4].copy()
+        for name in ("pattern", "resident"):
+            lk = TreeLikelihood(prob["tipcodes"], prob["weights"], prob["peel0"], prob["rooted"], prob["model"],
+                                C, max_draws=4, device=local)
+            lk.set_output(compact=True)
+            try:
+                lk.set_engine(name)
+            except Exception:  # the resident sweep refuses trees that do not fit (e.g. unrooted DS1)
+                sampler[name + "_us_per_call"] = None
+                lk.close()
+                continue
+            for _ in range(20):
+                lk.evaluate_rows(bl4, mv4)
+            ta = time.perf_counter()
+            for _ in range(200):
+                lk.evaluate_rows(bl4, mv4)
+            sampler[name + "_us_per_call"] = 1e6 * (time.perf_counter() - ta) / 200
+            lk.close()
+
     if info["engine"] == "class":
         alg = class_algorithmic_bytes(C, info["class_classes"], info["class_stage"], info["class_staged"], draws)
         kernel_name = "class sweep: cls_fwd/cls_root/cls_red/cls_fix/cls_rev kernels, forward through reverse"
@@ -512,6 +541,7 @@ def main():
             "host_inclusive": host_inclusive,
             "nominal_check": check,
             "single_eval": single,
+            "sampler_latency": sampler,
             "program": info,
             "kernel_source": kernel_source_hash(),
         }
