@@ -139,8 +139,11 @@ def compile_artifact(spec, script):
 
 def load_artifact(script):
     path = artifact_path(script)
-    with open(path) as fp:
-        doc = json.load(fp)
+    try:
+        with open(path) as fp:
+            doc = json.load(fp)
+    except (ValueError, UnicodeDecodeError):  # e.g. a real pystan pickle left at that path
+        raise SystemExit("%s is not a compiled-model artifact of this engine" % path)
     if not isinstance(doc, dict) or doc.get("phylostan_amd_compiled") != 1:
         raise SystemExit("%s is not a compiled-model artifact of this engine" % path)
     from . import _lib
@@ -217,7 +220,7 @@ def run(arg, likelihood_factory=None, log=print):
         # only --heterochronous puts lowers / lower_root into the model's data
         # (phylostan.py:259-263): the model stays homochronous
         tree = TreeData(d.S, d.peel0, d.map, None, None)
-    post = Posterior(spec, tree, lik)
+    post = Posterior(spec, tree, lik, compact_rows=True)
     seed = arg.seed if arg.seed is not None else int(time.time()) % 100000
     rng = np.random.default_rng(seed)
     names = post.column_names()

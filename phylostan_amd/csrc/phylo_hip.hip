@@ -1555,6 +1555,7 @@ struct phy_ctx {
   int wg_budget, cols_pref, wg_cap, lds_budget;
   int cu_count = 256, wg_resident = 512;  // resident workgroups of the current plan
   int K = 1;                   // columns per lane of the current plan
+  int hmax = 1;                // most pattern blocks one workgroup runs at once (slot regions per workgroup)
   int cap_m = 0, nchunks = 0;  // current LDS plan
   int deep_pref = 0;           // deep stack: 0 automatic, 1 LDS, 2 global
   bool deep_lds = false;       // current plan keeps the whole deep stack in LDS
@@ -2199,26 +2200,33 @@ int launch_pattern(phy_ctx* ctx, int n, const double* d_blens, const double* d_m
 }
 
 // Per-workgroup regions of the pattern sweep for `cap` workgroup slots:
-// moved-partial scratch, global deep entries, dL/dP and scalar slots.
+// moved-partial scratch, global deep entries, dL/dP and scalar slots.  The
+// new regions are allocated first and swapped in only when all four
+// succeed, so a failed grow leaves the context's current regions (and its
+// wg_cap) valid.
 int alloc_wg_buffers(phy_ctx* c, long cap) {
-  double2** d2[] = {&c->d_scratch, &c->d_dstk};
-  for (double2** b : d2)
-    if (*b) {
-      (void)hipFree(*b);
-      *b = nullptr;
-    }
-  double** d1[] = {&c->d_gslot, &c->d_sslot};
-  for (double** b : d1)
-    if (*b) {
-      (void)hipFree(*b);
-      *b = nullptr;
-    }
   const size_t ncolwg = (size_t)c->C * WAVE;
-  int rc = dalloc(&c->d_scratch, (size_t)cap * std::max(c->nslots, 1) * 2 * 2 * ncolwg);
-  if (!rc) rc = dalloc(&c->d_dstk, (size_t)cap * std::max(c->ndeep, 1) * 2 * 2 * ncolwg);
-  if (!rc) rc = dalloc(&c->d_gslot, (size_t)cap * c->C * c->nmat * 16);
-  if (!rc) rc = dalloc(&c->d_sslot, (size_t)cap * c->C * 8);
-  return rc;
+  double2 *scr = nullptr, *dsk = nullptr;
+  double *gsl = nullptr, *ssl = nullptr;
+  int rc = dalloc(&scr, (size_t)cap * std::max(c->nslots, 1) * 2 * 2 * ncolwg);
+  if (!rc) rc = dalloc(&dsk, (size_t)cap * std::max(c->ndeep, 1) * 2 * 2 * ncolwg);
+  if (!rc) rc = dalloc(&gsl, (size_t)cap * c->C * c->nmat * 16 * std::max(c->hmax, 1));
+  if (!rc) rc = dalloc(&ssl, (size_t)cap * c->C * 8 * std::max(c->hmax, 1));
+  if (rc) {
+    const std::string msg = g_err;
+    void* ps[] = {scr, dsk, gsl, ssl};
+    for (void* p : ps)
+      if (p) (void)hipFree(p);
+    return fail(rc, msg);
+  }
+  void* old[] = {c->d_scratch, c->d_dstk, c->d_gslot, c->d_sslot};
+  for (void* p : old)
+    if (p) (void)hipFree(p);
+  c->d_scratch = scr;
+  c->d_dstk = dsk;
+  c->d_gslot = gsl;
+  c->d_sslot = ssl;
+  return PHY_OK;
 }
 
 }  // namespace
@@ -2431,6 +2439,8 @@ int phy_output_len(const phy_ctx* ctx) {
 
 int phy_set_output(phy_ctx* ctx, int compact) {
   if (!ctx) return fail(PHY_EINVAL, "NULL ctx");
+  if (ctx->pending)  // phy_eval_wait copies rows of the submitted layout
+    return fail(PHY_EINVAL, "phy_set_output: a phy_eval_submit is still in flight (phy_eval_wait first)");
   HIP_TRY(hipSetDevice(ctx->device));
   HIP_TRY(hipStreamSynchronize(ctx->stream));
   if (compact && !ctx->d_grows) {

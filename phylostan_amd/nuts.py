@@ -331,7 +331,9 @@ class StaticHMCChain(Chain):
         h = self._H(z)
         if math.isnan(h):
             h = math.inf
-        accept = math.exp(H0 - h) if h != math.inf else 0.0
+        # Stan: accept_prob = exp(H0 - h) (inf when the energy drops by more
+        # than ~709 nats, i.e. accepted); math.exp would overflow there
+        accept = 0.0 if h == math.inf else (1.0 if H0 - h > 0 else math.exp(H0 - h))
         if accept < 1.0 and self.rng.uniform() > accept:
             z = z_init
         accept = min(1.0, accept)
@@ -358,8 +360,10 @@ class StaticHMCChain(Chain):
                     self._update_L()
                     self._da_restart()
                 if it == self.num_warmup - 1:
-                    self.eps = math.exp(self.x_bar)  # complete_adaptation
-                    self._update_L()
+                    # disengage_adaptation -> complete_adaptation(nom_epsilon) only:
+                    # sampling keeps the L of the last warmup update, as Stan's
+                    # adapt_diag_e_static_hmc does (no update_L_ there)
+                    self.eps = math.exp(self.x_bar)
             if it % self.thin == 0:
                 self.draws.append((z.q.copy(), z.lp, accept, eps_used, int_time, n_lf, 0, energy, warm))
         return self

@@ -135,15 +135,18 @@ class Posterior:
 
     ``likelihood`` is any object with ``evaluate_batch(blens [n,B],
     model_vecs [n,10+2C]) -> [EvalResult]`` -- the GPU ``TreeLikelihood`` in
-    the product.
+    the product.  ``compact_rows=True`` switches that likelihood to compact
+    output rows (``set_output(compact=True)``: no dL/dP block, which the
+    posterior never reads) -- a change to the caller's object, so it is
+    opt-in; the CLI and the samplers' drivers ask for it.
     """
 
-    def __init__(self, spec, tree, likelihood):
+    def __init__(self, spec, tree, likelihood, compact_rows=False):
         self.spec = spec
         self.tree = tree
         self.lik = likelihood
-        if hasattr(likelihood, "set_output"):
-            likelihood.set_output(compact=True)  # the sampler needs no dL/dP block
+        if compact_rows and hasattr(likelihood, "set_output"):
+            likelihood.set_output(compact=True)
         S = tree.S
         self.S = S
         self.C = spec.C

@@ -43,6 +43,23 @@ def phylo_case(point):
                 True, point["model"], 1, point["blens"], point["freqs"], point["rates"], [1.0], [1.0])
 
 
+def load_mixture_points():
+    """The configs' own variants evaluated by the reference's scripts/phylo.py
+    (tests/golden/make_golden.py ``mixture_fixture``): fluA HKY+W4 and HCV
+    GTR+W4 (C = 4 Weibull mixture) and DS1 JC69 unrooted (merged root edge)."""
+    with open(os.path.join(GOLDEN, "phylo_mixture.json")) as fp:
+        return json.load(fp)["points"]
+
+
+def mixture_case(point):
+    d = load_layout(point["dataset"])
+    S = d["tipbits"].shape[0]
+    B = 2 * S - 2 if point["rooted"] else 2 * S - 3
+    return Case("ref_%s_%s" % (point["dataset"], point["model"]), d["tipbits"], d["weights"], d["peel"] - 1,
+                point["rooted"], point["model"], point["C"], point["blens"][:B], point["freqs"], point["rates"],
+                point["rs"], point["ps"])
+
+
 class Case:
     """One likelihood problem in C-ABI conventions."""
 

@@ -214,7 +214,125 @@ def phylo_gtr_fixture(utils, phylo, specs):
     return out
 
 
+def _phylo_root_site_lik(phylo, tree, alignment, gtr):
+    """Per-site likelihoods L_i = sum_j pi_j p_root[i][j] from the
+    reference's own post-order traversal (compute_likelihood :283-290)."""
+    S = len(alignment)
+    phylo.setup_indexes(tree, alignment)
+    gtr.update()
+    partials = phylo.initialize_dna_partials(alignment)
+    matrices = np.zeros((2 * S - 2, 4, 4))
+    phylo.traverse(tree.seed_node, matrices, partials, gtr)
+    root = partials[2 * S - 2]
+    return np.array([sum(root[i][j] * gtr.get_pi(j) for j in range(4)) for i in range(alignment.sequence_size)])
+
+
+# The configs' own variants: the C = 4 Weibull mixture (fluA HKY+W4 at the
+# README point, HCV GTR+W4 at SConstruct:218's) and DS1's unrooted JC69.
+MIXTURE_POINTS = [
+    # dataset, model, exchangeabilities, freqs (None = empirical), clock rate, Weibull shape
+    ("fluA", "HKY", [1.0, 5.58, 1.0, 1.0, 5.58, 1.0], None, 0.00499, 0.488),
+    ("HCV", "GTR", [0.125, 0.25, 0.125, 0.125, 0.25, 0.125], [0.25] * 4, 7.9e-4, 0.5),
+]
+
+
+def mixture_fixture(phylo, specs):
+    """C = 4 Weibull mixtures and the unrooted merged-root-branch variant
+    through the reference's scripts/phylo.py pruner.
+
+    * Mixture (generate_script.py:998-1011): the reference pruner runs once
+      per category with every edge scaled by r_c (P(b r_c), :876-880), and the
+      per-site category likelihoods are combined as log sum_c ps_c L_c,i --
+      the one line of :1006-1010 restated here; r_c, ps_c are the median
+      Weibull categories of :267-278 (phylostan_amd.models.weibull_site_rates,
+      itself checked against the literal restatement in tests/test_oracle.py).
+    * DS1 (generate_script.py:1013-1023): the emitted code applies the root's
+      first child's matrix only (the root branch merged into it) and uses
+      node 2S-3's partials directly.  Under a reversible model the pulley
+      principle makes that the likelihood of the rooted tree whose edge to
+      node 2S-3 has length 0, so phylo.GTR([1]*6, [.25]*4) -- normalised JC69
+      -- evaluates it on the resolved DS1 tree with that edge zeroed and
+      blens ~ Exp(10) (seed 0, generate_script.py:1404) elsewhere.
+    """
+    from phylostan_amd import data, models
+    out = {"source": "scripts/phylo.py:4-61 (GTR), :240-296 (traverse); mixture log sum_c ps_c L_c "
+                     "(generate_script.py:1006-1010); unrooted = rooted with a zero root-edge to node 2S-3 "
+                     "(generate_script.py:1019, pulley principle)", "points": []}
+
+    def pattern_values(rows, taxa, site):
+        chars = np.array([[ord(ch) for ch in str(rows[t]).upper()] for t in taxa], dtype=np.uint8)
+        _, _, first = data.compress_patterns(chars)
+        return site[first]
+
+    for name, model, rates, freqs, clock, shape in MIXTURE_POINTS:
+        tpath, apath = specs[name][:2]
+        layout = np.load(os.path.join(HERE, "%s_layout.npz" % name), allow_pickle=False)
+        if freqs is None:
+            freqs = models.empirical_frequencies(layout["tipbits"], layout["weights"]).tolist()
+        rs, ps = models.weibull_site_rates(shape, 4)
+        aln = treeio.read_alignment(apath)
+        lik = []
+        for c in range(4):
+            tree = treeio.read_tree(tpath)
+            tree.resolve_polytomies(update_bipartitions=True)
+            rows = {t.label: _Seq(aln[t.label]) for t in tree.taxon_namespace}
+            alignment = _Alignment(rows)
+            for nd in tree.postorder_node_iter():
+                if nd.parent_node is not None:
+                    nd.edge_length = nd.edge_length * clock * rs[c]
+            lik.append(_phylo_root_site_lik(phylo, tree, alignment, phylo.GTR(list(rates), list(freqs))))
+        site = np.log(sum(ps[c] * lik[c] for c in range(4)))
+        taxa = [t.label for t in tree.taxon_namespace]
+        S = len(taxa)
+        blens = np.zeros(2 * S - 2)
+        tree = treeio.read_tree(tpath)
+        tree.resolve_polytomies(update_bipartitions=True)
+        phylo.setup_indexes(tree, _Alignment({t.label: _Seq(aln[t.label]) for t in tree.taxon_namespace}))
+        for nd in tree.postorder_node_iter():
+            if nd.parent_node is not None:
+                blens[nd.index] = nd.edge_length * clock
+        out["points"].append({"dataset": name, "model": model, "rooted": True, "C": 4, "rates": list(rates),
+                              "freqs": list(freqs), "rs": list(rs), "ps": list(ps), "clock_rate": clock,
+                              "wshape": shape, "loglik": float(np.sum(site)),
+                              "site_ll": pattern_values(rows, taxa, site).tolist(), "blens": blens.tolist()})
+        print(name, model, "+W4 reference mixture loglik %.10f" % np.sum(site))
+    # DS1 JC69 unrooted
+    tpath, apath = specs["DS1"][:2]
+    tree = treeio.read_tree(tpath)
+    tree.resolve_polytomies(update_bipartitions=True)
+    aln = treeio.read_alignment(apath)
+    rows = {t.label: _Seq(aln[t.label]) for t in tree.taxon_namespace}
+    alignment = _Alignment(rows)
+    S = len(alignment)
+    phylo.setup_indexes(tree, alignment)
+    layout = np.load(os.path.join(HERE, "DS1_layout.npz"), allow_pickle=False)
+    peel0 = layout["peel"] - 1
+    assert peel0[-1][1] == 2 * S - 3
+    blens = np.random.default_rng(0).exponential(1.0 / 10.0, size=2 * S - 3)  # tests/cases.py ds1_case(0)
+    for nd in tree.postorder_node_iter():
+        if nd.parent_node is not None:
+            nd.edge_length = 0.0 if nd.index == 2 * S - 3 else float(blens[nd.index])
+    # the merged branch: phylo's root children are peel0[-1][:2]
+    root_children = sorted(c.index for c in tree.seed_node.child_node_iter())
+    assert root_children == sorted(peel0[-1][:2].tolist()), (root_children, peel0[-1])
+    site = np.log(_phylo_root_site_lik(phylo, tree, alignment, phylo.GTR([1.0] * 6, [0.25] * 4)))
+    taxa = [t.label for t in tree.taxon_namespace]
+    out["points"].append({"dataset": "DS1", "model": "JC69", "rooted": False, "C": 1, "rates": [1.0] * 6,
+                          "freqs": [0.25] * 4, "rs": [1.0], "ps": [1.0], "loglik": float(np.sum(site)),
+                          "site_ll": pattern_values(rows, taxa, site).tolist(), "blens": blens.tolist()})
+    print("DS1 JC69 unrooted reference loglik %.10f" % np.sum(site))
+    return out
+
+
 def main():
+    if len(sys.argv) > 1 and sys.argv[1] == "mixture":  # only the mixture / unrooted fixture
+        ex = os.path.join(REF, "examples")
+        specs = {"fluA": (os.path.join(ex, "fluA", "fluA.tree"), os.path.join(ex, "fluA", "fluA.fa")),
+                 "HCV": (os.path.join(ex, "HCV", "HCV.tree"), os.path.join(ex, "HCV", "HCV.nexus")),
+                 "DS1": (os.path.join(ex, "DS1", "DS1.trees"), os.path.join(ex, "DS1", "DS1.nex"))}
+        with open(os.path.join(HERE, "phylo_mixture.json"), "w") as fp:
+            json.dump(mixture_fixture(_import_reference_phylo(), specs), fp)
+        return
     with open(os.path.join(HERE, "kat_3tax.json"), "w") as fp:
         json.dump(kat_fixture(), fp, indent=1)
     utils = _import_reference_utils()
@@ -228,8 +346,11 @@ def main():
         fx = layout_fixture(utils, tpath, apath, het, rooted)
         np.savez_compressed(os.path.join(HERE, "%s_layout.npz" % name), **fx)
         print(name, "S=%d P=%d sites=%d" % (fx["tipbits"].shape[0], fx["tipbits"].shape[1], fx["sites"]))
+    phylo = _import_reference_phylo()
     with open(os.path.join(HERE, "phylo_gtr.json"), "w") as fp:
-        json.dump(phylo_gtr_fixture(utils, _import_reference_phylo(), specs), fp)
+        json.dump(phylo_gtr_fixture(utils, phylo, specs), fp)
+    with open(os.path.join(HERE, "phylo_mixture.json"), "w") as fp:
+        json.dump(mixture_fixture(phylo, specs), fp)
 
 
 if __name__ == "__main__":

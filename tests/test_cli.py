@@ -231,3 +231,8 @@ def test_compiled_model_artifact(tmp_path):
     doc = cli.load_artifact(script)
     assert doc["options"]["model"] == "HKY" and doc["options"]["categories"] == 4
     json.loads(open(str(tmp_path / "m.pkl")).read())  # JSON, never a pickle
+    # a real pystan pickle (binary) at that path is refused cleanly, never unpickled
+    with open(str(tmp_path / "p.pkl"), "wb") as fp:
+        fp.write(b"\x80\x04\x95\x10\x00\x00\x00\x00\x00\x00\x00\xff\xfe")
+    with pytest.raises(SystemExit):
+        cli.load_artifact(str(tmp_path / "p.stan"))

@@ -104,32 +104,6 @@ def test_class_sweep_deterministic_and_agrees_with_pattern_sweep():
     _close(a.dLdP, c.dLdP, RTOL_G, "dLdP")
 
 
-def test_class_sweep_synthetic_200k_vs_c_port():
-    """The synthetic workload at 200k sites (121k patterns): the automatic
-    choice is the class sweep; against the OpenMP C port."""
-    import os
-    from oracle import cpu
-    from phylostan_amd import synthetic
-    from phylostan_amd.engine import EvalResult
-    pd, prm = synthetic.simulate(n_sites=200_000)
-    case = cases.Case("syn200k", pd.tipcodes, pd.weights, pd.peel0, True, "GTR", 4, prm["blens"], prm["freqs"],
-                      prm["rates"], prm["rs"], prm["ps"])
-    eng = _engine(case)
-    assert eng.engine() == "class"
-    res = eng.evaluate(case.blens, case.model_vec(), site_ll=True)
-    nt = max(1, min(16, os.cpu_count() or 1))
-    out, sl = cpu.evaluate(case.tipcodes, case.weights, case.peel0, True, 2, case.model_vec(), case.blens, 4,
-                           site_ll=True, nthreads=nt)
-    ref = EvalResult(out, eng.B, 4, sl)
-    np.testing.assert_allclose(res.site_ll, ref.site_ll, rtol=RTOL_LL, atol=1e-12)
-    assert abs(res.loglik - ref.loglik) <= RTOL_LL * abs(ref.loglik)
-    _close(res.dLdP, ref.dLdP, RTOL_G, "dLdP")
-    _close(res.grad_blens, ref.grad_blens, RTOL_G, "grad_blens")
-    _close(res.grad_rs, ref.grad_rs, RTOL_G, "grad_rs")
-    _close(res.grad_ps, ref.grad_ps, RTOL_G, "grad_ps")
-    _close(res.grad_freq_root, ref.grad_freq_root, RTOL_G, "grad_freq_root")
-
-
 def _with_clade(case, value, max_draws=1):
     import os
     old = os.environ.get("PHY_CLADE")

@@ -54,23 +54,6 @@ def check_case(case, eng=None, res=None):
     return res
 
 
-def test_kat_3tax_reference_values():
-    """The reference's only known-answer test (eigen/test_ll_3tax.py)."""
-    kat = cases.load_kat()
-    for pt in kat["points"]:
-        case = cases.kat_case(pt)
-        res = check_case(case)
-        assert abs(res.loglik - pt["loglik"]) < 1e-12
-        g = res.grad_blens * 0.75  # d/dt of the unnormalised-Q formula
-        np.testing.assert_allclose(g[[0, 1, 3, 2]], pt["grad_fd"], rtol=1e-6)
-
-
-@pytest.mark.parametrize("make", [cases.fluA_case, cases.hcv_case, cases.ds1_case],
-                         ids=["fluA_HKY_W4", "HCV_GTR_W4", "DS1_JC69_unrooted"])
-def test_config_datasets(make):
-    check_case(make())
-
-
 @pytest.mark.parametrize("seed,S,P,C,model,rooted,cat", [
     (1, 5, 1, 1, "JC69", True, False),       # single pattern
     (2, 12, 63, 3, "GTR", True, False),      # P < one block
@@ -369,51 +352,6 @@ def test_many_categories(C):
     eng = _engine(case)
     assert eng.lds_plan()["cols"] == 1
     check_case(case, eng)
-
-
-@pytest.mark.parametrize("k", range(4))
-def test_reference_phylo_py_points(k):
-    """HKY / GTR through the eigen path against the reference's own pruner
-    (scripts/phylo.py, tests/golden/phylo_gtr.json): per-pattern and total
-    log-likelihoods."""
-    pt = cases.load_phylo_points()[k]
-    case = cases.phylo_case(pt)
-    res = check_case(case)
-    np.testing.assert_allclose(res.site_ll, pt["site_ll"], rtol=RTOL_LL, atol=1e-12)
-    assert abs(res.loglik - pt["loglik"]) <= RTOL_LL * abs(pt["loglik"])
-
-
-def test_synthetic_full_size_vs_c_port():
-    """BASELINE config 4 at its full size: 128 taxa x 1,000,000 simulated
-    sites (528,111 patterns), GTR+W4 at the simulation's own parameters.  The
-    plan this hits is the bench's: thousands of pattern blocks on persistent
-    workgroups, several LDS chunks, and the multi-workgroup dL/dP sum.  The
-    GPU is compared with the OpenMP C port (per-site log L rel 1e-10,
-    gradients 1e-9)."""
-    import os
-    from oracle import cpu
-    from phylostan_amd import synthetic
-    from phylostan_amd.engine import EvalResult
-    pd, prm = synthetic.simulate(n_sites=1_000_000)
-    case = cases.Case("synthetic", pd.tipcodes, pd.weights, pd.peel0, True, "GTR", 4, prm["blens"],
-                      prm["freqs"], prm["rates"], prm["rs"], prm["ps"])
-    assert case.P == 528111
-    eng = _engine(case)
-    info = eng.program_info()
-    plan = eng.lds_plan()
-    assert info["nblocks"] > 4000 and plan["n_chunks"] > 1
-    res = eng.evaluate(case.blens, case.model_vec(), site_ll=True)
-    nt = max(1, min(16, os.cpu_count() or 1))
-    out, sl = cpu.evaluate(case.tipcodes, case.weights, case.peel0, True, 2, case.model_vec(), case.blens, 4,
-                           site_ll=True, nthreads=nt)
-    ref = EvalResult(out, eng.B, 4, sl)
-    np.testing.assert_allclose(res.site_ll, ref.site_ll, rtol=RTOL_LL, atol=1e-12)
-    assert abs(res.loglik - ref.loglik) <= RTOL_LL * abs(ref.loglik)
-    _close(res.dLdP, ref.dLdP, RTOL_G, "dLdP")
-    _close(res.grad_blens, ref.grad_blens, RTOL_G, "grad_blens")
-    _close(res.grad_rs, ref.grad_rs, RTOL_G, "grad_rs")
-    _close(res.grad_ps, ref.grad_ps, RTOL_G, "grad_ps")
-    _close(res.grad_freq_root, ref.grad_freq_root, RTOL_G, "grad_freq_root")
 
 
 @pytest.mark.parametrize("engine", ["pattern", "class"])

@@ -208,3 +208,22 @@ def test_oracle_vs_reference_phylo_py(k):
                            case.model_vec(), case.blens, 1, site_ll=True)
     np.testing.assert_allclose(sl, pt["site_ll"], rtol=1e-10, atol=1e-12)
     assert abs(out[0] - pt["loglik"]) <= 1e-10 * abs(pt["loglik"])
+
+
+@pytest.mark.parametrize("k", range(3), ids=["fluA_HKY_W4", "HCV_GTR_W4", "DS1_JC69_unrooted"])
+def test_oracle_vs_reference_mixture_and_unrooted(k):
+    """The configs' own variants pinned to the reference's scripts/phylo.py
+    (tests/golden/phylo_mixture.json): the C = 4 Weibull mixture of fluA /
+    HCV (generate_script.py:998-1011) and DS1's unrooted merged root branch
+    (:1013-1023).  Oracle (numpy and C) per-pattern and total log L at rel
+    1e-10 (all-gap patterns, log L ~ 0, at abs 1e-12)."""
+    from oracle import cpu
+    pt = cases.load_mixture_points()[k]
+    case = cases.mixture_case(pt)
+    ref = case.oracle()
+    np.testing.assert_allclose(ref["site_ll"], pt["site_ll"], rtol=1e-10, atol=1e-12)
+    assert abs(ref["loglik"] - pt["loglik"]) <= 1e-10 * abs(pt["loglik"])
+    out, sl = cpu.evaluate(case.tipcodes, case.weights, case.peel0, case.rooted, npr.MODEL_IDS[case.model],
+                           case.model_vec(), case.blens, case.C, site_ll=True)
+    np.testing.assert_allclose(sl, pt["site_ll"], rtol=1e-10, atol=1e-12)
+    assert abs(out[0] - pt["loglik"]) <= 1e-10 * abs(pt["loglik"])

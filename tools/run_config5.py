@@ -53,7 +53,7 @@ def main():
             lik.prefer_latency_engine()
         elif a.engine != "auto":
             lik.set_engine(a.engine)
-        return Posterior(spec, tree, lik)
+        return Posterior(spec, tree, lik, compact_rows=True)
     post = make_post()
     lik = post.lik
     posts = [post] + [make_post() for _ in range(a.groups - 1)]  # pipelined chain groups (nuts.run_chains)
