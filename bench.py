@@ -443,31 +443,46 @@ def main():
         tb = time.perf_counter()
         single = dict(evals_per_s=n1 / (tb - ta), us_per_eval=1e6 * (tb - ta) / n1)
 
-    # the sampler path (host buffers, 4 draws per call, compact rows): µs per
-    # call on the pattern sweep and on the resident class sweep, which the
-    # CLI's NUTS / HMC / ADVI contexts use when it applies
-    sampler = None
+    # the sampler path (host buffers, compact rows -- what phylostan run
+    # issues): µs per call of 4 draws (NUTS, one draw per chain) and the
+    # evals/s of ADVI's ELBO estimate, elbo_samples = 100 draws per call
+    # (phylostan.py:47), on the pattern sweep (one kernel launch per call,
+    # DESIGN.md 5) and on the resident class sweep
+    sampler = draws_100 = None
     if batched and rank == 0 and world == 1 and not args.no_sampler_latency:
         from phylostan_amd.engine import TreeLikelihood
         sampler = {"draws_per_call": 4}
-        bl4 = blens[0][:4].copy()
-        mv4 = mvs[0][:4].copy()
+        draws_100 = {"draws_per_call": 100, "unit": "evals/s",
+                     "note": "ADVI's ELBO estimate (elbo_samples = 100, phylostan.py:47): host buffers in, "
+                             "compact rows out, one synchronous call each"}
+        bl4, mv4 = blens[0][:4].copy(), mvs[0][:4].copy()
+        bl100 = np.concatenate([blens[0]] * (1 + 100 // draws))[:100].copy()
+        mv100 = np.concatenate([mvs[0]] * (1 + 100 // draws))[:100].copy()
         for name in ("pattern", "resident"):
             lk = TreeLikelihood(prob["tipcodes"], prob["weights"], prob["peel0"], prob["rooted"], prob["model"],
-                                C, max_draws=4, device=local)
+                                C, max_draws=100, device=local)
             lk.set_output(compact=True)
             try:
                 lk.set_engine(name)
             except Exception:  # the resident sweep refuses trees that do not fit (e.g. unrooted DS1)
                 sampler[name + "_us_per_call"] = None
+                draws_100[name] = None
                 lk.close()
                 continue
             for _ in range(20):
                 lk.evaluate_rows(bl4, mv4)
             ta = time.perf_counter()
-            for _ in range(200):
+            for _ in range(300):
                 lk.evaluate_rows(bl4, mv4)
-            sampler[name + "_us_per_call"] = 1e6 * (time.perf_counter() - ta) / 200
+            sampler[name + "_us_per_call"] = 1e6 * (time.perf_counter() - ta) / 300
+            for _ in range(5):
+                lk.evaluate_rows(bl100, mv100)
+            ta = time.perf_counter()
+            for _ in range(100):
+                lk.evaluate_rows(bl100, mv100)
+            el100 = (time.perf_counter() - ta) / 100
+            draws_100[name] = 100 / el100
+            draws_100[name + "_us_per_call"] = 1e6 * el100
             lk.close()
 
     if info["engine"] == "class":
@@ -542,6 +557,7 @@ def main():
             "nominal_check": check,
             "single_eval": single,
             "sampler_latency": sampler,
+            "draws_100": draws_100,
             "program": info,
             "kernel_source": kernel_source_hash(),
         }

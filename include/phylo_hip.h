@@ -93,6 +93,26 @@ int phy_create(int S, int P, int C, int rooted, int model,
                const uint8_t* tipcodes, const double* weights, const int32_t* peel,
                int max_draws, int device, phy_ctx** out);
 
+/* One context over several devices (phy_create's n_dev; 8e:
+ * single-process multi-device with RCCL inside the context).  The P
+ * patterns are split into n_shards contiguous ranges of whole 128-pattern
+ * blocks (counts differ by <= 1), shard k a full context on devices[k].  An
+ * evaluation runs every shard on its own stream, then reduces the fp64
+ * output rows once: ncclAllReduce(sum) over the shards' communicators
+ * (ncclCommInitAll; RCCL is loaded on first use) when the devices are all
+ * distinct, a device-side sum in shard order when they are all the same
+ * (any other mix is PHY_EINVAL).  Rows equal the single-context rows to
+ * rounding (every entry is a sum over patterns); site log-likelihoods are
+ * gathered into [n][P] by phy_eval.  phy_eval, phy_eval_submit / wait,
+ * phy_pruning_loglik, phy_eval_device (buffers on devices[0], no site_ll),
+ * phy_set_output / engine / tuning (applied to every shard) and the info
+ * queries (shard 0) accept the returned handle; phy_destroy frees it all.
+ * The reference's boundary is one synchronous call per log_prob
+ * (eigen/prune_stan.hpp:9-17): this is how that single handle reaches a
+ * whole node. */
+int phy_create_multi(int S, int P, int C, int rooted, int model, const uint8_t* tipcodes, const double* weights,
+                     const int32_t* peel, int max_draws, int n_shards, const int* devices, phy_ctx** out);
+
 int phy_destroy(phy_ctx* ctx);
 
 /* Message of the last failure on this thread ("" if none). */
@@ -118,15 +138,20 @@ int phy_eval_device(phy_ctx* ctx, int n_draws, const double* d_blens, const doub
                     double* d_out, double* d_site_ll, void* stream);
 
 /* Asynchronous small batches (host buffers, 1 <= n_draws <= min(max_draws,
- * 64)): phy_eval_submit copies the inputs into the context's pinned staging
- * and queues the upload, the evaluation and the download of the output rows
- * on the context's stream, then returns; phy_eval_wait blocks until they are
- * done and copies the n_draws rows (phy_output_len doubles each) into `out`.
- * One submission in flight per context (phy_eval refuses while one is);
- * contexts on one device run concurrently, so a sampler can overlap one
- * group of chains' host work with another group's evaluation.  phy_eval is
- * submit + wait (plus site log-likelihoods).  No reference counterpart: the
- * reference's log_prob is synchronous (eigen/prune_stan.hpp:9-17). */
+ * 128)): phy_eval_submit queues the evaluation on the context's stream and
+ * returns; phy_eval_wait blocks until it is done and copies the n_draws rows
+ * (phy_output_len doubles each) into `out`.  When one workgroup per draw
+ * runs the whole pattern sweep (the sampler-sized configs: fluA, HCV, DS1)
+ * this is a SINGLE kernel launch: the inputs and their host-computed
+ * eigensystems go into the context's pinned staging, which the sweep reads
+ * itself; it builds the matrix records, sweeps, finalizes, applies the
+ * Q-parameter chain rule and writes the rows straight into pinned memory
+ * (no copies, no other kernels).  Otherwise: upload, the kernel sequence,
+ * download.  One submission in flight per context (phy_eval refuses while
+ * one is); contexts on one device run concurrently.  phy_eval takes the same
+ * path for n_draws <= 128 (plus site log-likelihoods).  No reference
+ * counterpart: the reference's log_prob is synchronous
+ * (eigen/prune_stan.hpp:9-17). */
 int phy_eval_submit(phy_ctx* ctx, int n_draws, const double* blens, const double* model);
 int phy_eval_wait(phy_ctx* ctx, double* out);
 

@@ -24,6 +24,9 @@ SIGNATURES = {
     "phy_create": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                   ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int,
                                   ctypes.c_int, ctypes.POINTER(ctypes.c_void_p)]),
+    "phy_create_multi": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                        ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int,
+                                        ctypes.c_int, ctypes.c_void_p, ctypes.POINTER(ctypes.c_void_p)]),
     "phy_destroy": (ctypes.c_int, [ctypes.c_void_p]),
     "phy_last_error": (ctypes.c_char_p, []),
     "phy_num_branches": (ctypes.c_int, [ctypes.c_void_p]),

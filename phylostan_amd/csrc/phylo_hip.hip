@@ -266,10 +266,10 @@ struct SweepArgs {
   const double* weights;  // [Ppad]   (0 on padding)
   const double* pmat;     // [draw][C][nmat][R][4]  matrix records, program-use order
   const double* model;    // [draw][10+2C]
-  double2* scratch;       // [wg][nslots][K][2][C*64]  stored moved partials
-  double2* dstk;          // [wg][ndeep][K][2][C*64]   deep-stack entries
-  double* gslot;          // [wg][C][nmat][16]  dL/dP partial sums (per-wave atomic adds)
-  double* sslot;          // [wg][C][8]
+  double2* scratch;       // [region][nslots][K][2][C*64]  stored moved partials
+  double2* dstk;          // [region][ndeep][K][2][C*64]   deep-stack entries
+  double* gslot;          // [region][C][nmat][16]  dL/dP partial sums (per-wave store / atomic adds)
+  double* sslot;          // [region][C][8]
   double* site_ll;        // [draw][P] or null
   double* out;            // [draw][outlen]: dL/dP rows written in place when g_direct
   const int* mat_branch;  // [nmat] branch of matrix m
@@ -282,25 +282,49 @@ struct SweepArgs {
   const double* blens;  // [draw][B] (fin)
   double* grows;        // dL/dP rows of draw d at grows + d * grows_stride (in `out`, or scratch when compact)
   long long grows_stride;
+  // H pattern blocks per workgroup pass: wave w = h*C + c runs category c of
+  // block h; the H waves of a category share its LDS matrix chunk.  A
+  // "region" (scratch, deep stack, dL/dP and scalar slots) belongs to one
+  // (workgroup, h): region = wg*H + h.
+  int H;
+  unsigned padw;  // eight padding nibbles (the record index of mask 15)
+  // Single-launch evaluation (pro, g_direct only): the workgroup first copies
+  // its draw's inputs from the caller's host-visible buffers (h_*) into the
+  // device buffers above (w_*) and builds the draw's matrix records
+  // (pmat_kernel's work); qfused: the Q-parameter chain rule (qgrad_kernel's
+  // work) runs after the finalize.
+  int pro, qfused, kind;
+  const double* h_blens;
+  const double* h_model;
+  const double* h_eig;
+  double* w_blens;
+  double* w_model;
+  double* w_eig;
+  double* w_pmat;
 };
 
-// LDS carve (16-B aligned pieces), K columns per lane:
-//   tips   S x 64K nibbles            record indices, shared by the C category waves
-//   mats   C x cap_m x R x 4 doubles  wave c's chunk of matrix records
+// LDS carve (16-B aligned pieces), K columns per lane, H blocks per pass:
+//   tips   S x H x 64K nibbles         record indices, shared by the C category waves
+//   mats   C x cap_m x R x 4 doubles  category c's chunk of matrix records
+//                                     (shared by its H waves)
 //   tail   per wave: ndl deep entries of K x 2 x 64 double2 (the deep
 //          entries [0, ndl) kept in LDS), or K x 64 doubles when ndl = 0;
-//          wave c's root-exchange slice (K x 64 doubles) sits at the start
+//          wave w's root-exchange slice (K x 64 doubles) sits at the start
 //          of its own tail, whose deep entries are all free at the root
-// tips: the block's nibbles, then the 0/1 state vectors of the 16 record
+// tips: the blocks' nibbles, then the 0/1 state vectors of the 16 record
 // indices (the t of dL/dP += r (x) t for a tip child: two LDS reads instead
 // of unpacking and converting its mask bits per column)
-__host__ __device__ inline size_t tip_nib_bytes(int S, int K) { return ((size_t)S * WAVE * K / 2 + 15) / 16 * 16; }
-__host__ __device__ inline size_t tip_lds_bytes(int S, int K) { return tip_nib_bytes(S, K) + 16 * 4 * sizeof(double); }
+__host__ __device__ inline size_t tip_nib_bytes(int S, int K, int H) {
+  return ((size_t)S * H * WAVE * K / 2 + 15) / 16 * 16;
+}
+__host__ __device__ inline size_t tip_lds_bytes(int S, int K, int H) {
+  return tip_nib_bytes(S, K, H) + 16 * 4 * sizeof(double);
+}
 __host__ __device__ inline size_t tail_doubles(int K, int ndl) {  // per wave
   return ndl > 0 ? (size_t)ndl * K * 2 * WAVE * 2 : (size_t)K * WAVE;
 }
-__host__ __device__ inline size_t lds_bytes(int S, int C, int R, int cap_m, int K, int ndl) {
-  return tip_lds_bytes(S, K) + (size_t)C * cap_m * R * 32 + (size_t)C * tail_doubles(K, ndl) * 8;
+__host__ __device__ inline size_t lds_bytes(int S, int C, int R, int cap_m, int K, int ndl, int H) {
+  return tip_lds_bytes(S, K, H) + (size_t)C * cap_m * R * 32 + (size_t)C * H * tail_doubles(K, ndl) * 8;
 }
 
 // Buffer resource over a workgroup's scratch / deep-stack region: loads past
@@ -454,6 +478,207 @@ __device__ __forceinline__ void build_record(const double* __restrict__ e, doubl
   }
 }
 
+// dlogL / d(exchangeabilities[6], freqs[4]) through the eigendecomposition:
+// the device form of models.q_param_gradients_batch (Q = V diag(lam) V^-1,
+// V = m1 = Pi^-1/2 U, V^-1 = m2 = U^T Pi^1/2, t = r_c b):
+//   H_cb = V^T G_cb V^-T,  Phi_cb[k][l] = (e^{lam_k t} - e^{lam_l t}) / (lam_k - lam_l)
+//   (t e^{lam_k t} on ties),  M = sum_cb H_cb .* Phi_cb,  W = V^-T M V^T,
+//   qw = <Q, W>,  s = the normaliser of Q (generate_script.py:862-868);
+//   rate (i,j): (f_j W_ij + f_i W_ji - f_j W_ii - f_i W_jj - 2 f_i f_j qw) / s
+//   freq m:     (sum_{j != m} R_jm (W_jm - W_jj) - qw sum_{j != m} 2 R_mj f_j) / s
+//               + the explicit root term.
+// One workgroup per draw; per-thread partial M over (c, b) (the per-draw
+// V, V^-1, lambda and 1/(lambda_k - lambda_l) in LDS, so a thread holds only
+// M, G and one row of V^T G: ~100 VGPRs instead of 200, twice the resident
+// waves), a wave reduction of the 16 partials, then the waves in order:
+// deterministic.  JC69 has no Q parameters: zeros.
+// qgrad_body: the work of a 256-thread workgroup (4 "virtual" waves; a
+// smaller workgroup runs them in turn, a larger one leaves its waves >= 4
+// idle), so qgrad_kernel and the sweep's fused epilogue give the same bits;
+// every thread of the workgroup must call it (it holds barriers).
+// sh: QG_SHARED doubles of LDS.
+struct QgArgs {
+  const double* eig;    // [draw][EIG_LEN]
+  const double* model;  // [draw][10+2C]
+  const double* blens;  // [draw][B]
+  const double* grows;  // dL/dP rows of draw d at grows + d * grows_stride
+  long long grows_stride;
+  double* out;          // [draw][outlen]
+  int outlen, C, B, kind;
+};
+constexpr int QG_THREADS = 256;
+constexpr int QG_SHARED = 16 * 3 + 4 + 4 * 16 + 16 * 2;  // V, V^-1, 1/(lam_k - lam_l), lam, wave partials, M, W
+__device__ void qgrad_body(const QgArgs& a, int draw, int tid, double* sh) {
+  double* sV = sh;
+  double* sVi = sh + 16;
+  double* srinv = sh + 32;
+  double* slam = sh + 48;
+  double* part = sh + 52;  // [4][16]
+  double* sM = sh + 116;
+  double* sW = sh + 132;
+  const int lane = tid & 63, wave = tid >> 6;
+  const int nwr = max(1, (int)(blockDim.x >> 6));  // the workgroup's waves
+  const int C = a.C, B = a.B;
+  double* out = a.out + (size_t)draw * a.outlen;
+  const int o = 1 + B + 2 * C;
+  if (a.kind == PHY_JC69) {  // workgroup-uniform
+    if (tid < 10) out[o + 4 + tid] = 0.0;
+    return;
+  }
+  const double* e = a.eig + (size_t)draw * EIG_LEN;
+  if (tid < 16) {
+    sV[tid] = e[EIG_M1 + tid];
+    sVi[tid] = e[EIG_M2 + tid];
+    // 1 / (lam_k - lam_l) once per draw (0 marks a tie: t e^{lam_k t} there)
+    const double lk = e[EIG_LAM + (tid >> 2)], ll = e[EIG_LAM + (tid & 3)];
+    const double d = lk - ll;
+    srinv[tid] = fabs(d) < 1e-12 * fmax(1.0, fabs(lk)) ? 0.0 : 1.0 / d;
+    if (tid < 4) slam[tid] = e[EIG_LAM + tid];
+  }
+  __syncthreads();
+  const double* mdl = a.model + (size_t)draw * (10 + 2 * C);
+  const double* bl = a.blens + (size_t)draw * B;
+  const double* rows = a.grows + (size_t)draw * a.grows_stride;
+  // a quad of lanes per (c, b): lane k forms row k of H = V^T G V^-T and
+  // accumulates row k of M (4 values); e^{lam_k t} comes from lane k
+  const int k = tid & 3;
+  for (int vw = wave; vw < QG_THREADS / 64; vw += nwr) {  // virtual wave vw: threads vw*64 + lane
+    const int vt = vw * 64 + lane;
+    double m[4] = {0.0, 0.0, 0.0, 0.0};
+    for (int idx = vt >> 2; idx < C * B; idx += QG_THREADS / 4) {
+      const int c = idx / B, b = idx - c * B;
+      const double t = mdl[10 + c] * bl[b];
+      double G[16];
+      const double2* g2 = reinterpret_cast<const double2*>(rows + (size_t)idx * 16);
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const double2 v = g2[u];
+        G[2 * u] = v.x;
+        G[2 * u + 1] = v.y;
+      }
+      const double Ek = exp(slam[k] * t);
+      double E[4];
+      E[0] = dpp_d<0x00>(Ek);
+      E[1] = dpp_d<0x55>(Ek);
+      E[2] = dpp_d<0xAA>(Ek);
+      E[3] = dpp_d<0xFF>(Ek);
+      double T[4];  // row k of V^T G
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        double acc = 0.0;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) acc = fma(sV[i * 4 + k], G[i * 4 + j], acc);
+        T[j] = acc;
+      }
+#pragma unroll
+      for (int l = 0; l < 4; ++l) {
+        double hh = 0.0;  // (V^T G V^-T)[k][l]
+#pragma unroll
+        for (int j = 0; j < 4; ++j) hh = fma(T[j], sVi[l * 4 + j], hh);
+        const double ri = srinv[k * 4 + l];
+        const double phi = ri == 0.0 ? t * Ek : (Ek - E[l]) * ri;
+        m[l] = fma(hh, phi, m[l]);
+      }
+    }
+    // sum over the wave's 16 quads (lane bits 2..5): lanes with bits 2, 3
+    // clear end with M[k][2 b5 + b4]
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      swap32(m[u], m[u + 2]);
+      m[u] += m[u + 2];
+    }
+    swap16(m[0], m[1]);
+    m[0] += m[1];
+    m[0] += dpp_d<DPP_ROW_ROR8>(m[0]);
+    m[0] += dpp_d<0x124>(m[0]);  // row_ror:4 (symmetric after the ror:8 stage)
+    if ((lane & 12) == 0) part[vw * 16 + k * 4 + ((lane >> 5) & 1) * 2 + ((lane >> 4) & 1)] = m[0];
+  }
+  __syncthreads();
+  // M = the waves' partials in order; W = V^-T M V^T, one entry per thread:
+  // W[i][j] = sum_kl Vi[k][i] M[k][l] V[j][l]
+  if (tid < 16) {
+    double acc = part[tid];
+    for (int w = 1; w < QG_THREADS / 64; ++w) acc += part[w * 16 + tid];
+    sM[tid] = acc;
+  }
+  __syncthreads();
+  if (tid < 16) {
+    const int i = tid >> 2, j = tid & 3;
+    double acc = 0.0;
+    for (int kk = 0; kk < 4; ++kk) {
+      double ml = 0.0;
+      for (int l = 0; l < 4; ++l) ml = fma(sM[kk * 4 + l], sV[j * 4 + l], ml);
+      acc = fma(sVi[kk * 4 + i], ml, acc);
+    }
+    sW[tid] = acc;
+  }
+  __syncthreads();
+  if (tid != 0) return;
+  double W[16];
+  for (int kk = 0; kk < 16; ++kk) W[kk] = sW[kk];
+  const double* Q = e + EIG_Q;
+  const double sn = e[EIG_S];
+  double qw = 0.0;
+#pragma unroll
+  for (int kk = 0; kk < 16; ++kk) qw = fma(Q[kk], W[kk], qw);
+  const double f[4] = {mdl[0], mdl[1], mdl[2], mdl[3]};
+  const double* r = mdl + 4;  // AC AG AT CG CT GT
+  const int pi_[6] = {0, 0, 0, 1, 1, 2}, pj_[6] = {1, 2, 3, 2, 3, 3};
+  double Rm[16];
+#pragma unroll
+  for (int kk = 0; kk < 16; ++kk) Rm[kk] = 0.0;
+#pragma unroll
+  for (int kk = 0; kk < 6; ++kk) {
+    const int i = pi_[kk], j = pj_[kk];
+    Rm[i * 4 + j] = Rm[j * 4 + i] = r[kk];
+    const double dq = f[j] * W[i * 4 + j] + f[i] * W[j * 4 + i] - f[j] * W[i * 4 + i] - f[i] * W[j * 4 + j];
+    out[o + 4 + kk] = (dq - 2.0 * f[i] * f[j] * qw) / sn;
+  }
+#pragma unroll
+  for (int mm = 0; mm < 4; ++mm) {
+    double dq = 0.0, ds = 0.0;
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      if (j != mm) {
+        dq += Rm[j * 4 + mm] * (W[j * 4 + mm] - W[j * 4 + j]);
+        ds += 2.0 * Rm[mm * 4 + j] * f[j];
+      }
+    out[o + 10 + mm] = (dq - ds * qw) / sn + out[o + mm];
+  }
+}
+
+// Single-launch evaluation (SweepArgs::pro, g_direct): the workgroup copies
+// its draw's inputs from the caller's host-visible staging into LDS and the
+// device buffers, then builds the draw's matrix records (pmat_kernel's work,
+// the same build_record).  A separate instantiation of the sweep (PRO):
+// compiled into the throughput kernels it costs registers across the step
+// loops (K = 2, deep stack in LDS: 239 -> 256 VGPRs and a spill).
+__device__ __forceinline__ void sweep_prologue(const SweepArgs& a, int draw, double* inL) {
+  const int C = a.C, nmat = a.nmat, nthreads = blockDim.x, rec = a.R * 4;
+  const int B = a.B, ML = 10 + 2 * C;  // inL: [B | ML | EIG_LEN]
+  for (int k = threadIdx.x; k < B + ML + EIG_LEN; k += nthreads) {
+    double v;
+    if (k < B) {
+      v = a.h_blens[(size_t)draw * B + k];
+      a.w_blens[(size_t)draw * B + k] = v;
+    } else if (k < B + ML) {
+      v = a.h_model[(size_t)draw * ML + (k - B)];
+      a.w_model[(size_t)draw * ML + (k - B)] = v;
+    } else {
+      v = a.h_eig[(size_t)draw * EIG_LEN + (k - B - ML)];
+      a.w_eig[(size_t)draw * EIG_LEN + (k - B - ML)] = v;
+    }
+    inL[k] = v;
+  }
+  __syncthreads();
+  for (int idx = threadIdx.x; idx < C * nmat; idx += nthreads) {
+    const int cc = idx / nmat, m = idx - cc * nmat;
+    build_record(inL + B + ML, inL[a.mat_branch[m]] * inL[B + 10 + cc], a.kind, a.R, a.extra,
+                 reinterpret_cast<double2*>(a.w_pmat + ((size_t)draw * C * nmat + idx) * rec));
+  }
+  __syncthreads();  // records and inputs visible to the workgroup; LDS free again
+}
+
 // The sweep.  `prog` is a separate __restrict__ const argument so the
 // backend proves it read-only and uses scalar loads.
 //
@@ -476,22 +701,27 @@ __device__ __forceinline__ void build_record(const double* __restrict__ e, doubl
 #ifndef PHY_WPE2
 #define PHY_WPE2 2  // waves per SIMD the K=2 kernel is register-budgeted for
 #endif
-template <int MAXT, int K, bool DL>
+template <int MAXT, int K, bool DL, bool PRO>
 __global__ void __launch_bounds__(MAXT) __attribute__((amdgpu_waves_per_eu(K == 2 ? PHY_WPE2 : 4)))
     sweep_kernel(SweepArgs a, const int* __restrict__ prog) {
   extern __shared__ __attribute__((aligned(16))) unsigned char lds_raw[];
   const int lane = threadIdx.x & (WAVE - 1);
-  const int c = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int C = a.C, nsteps = a.nsteps, nmat = a.nmat, H = a.H;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave = h * C + c
+  const int h = __builtin_amdgcn_readfirstlane(w / C);
+  const int c = w - h * C;
   const int nthreads = blockDim.x;
   const int draw = blockIdx.y;
   const int wg = blockIdx.y * gridDim.x + blockIdx.x;
-  const int C = a.C, nsteps = a.nsteps, nmat = a.nmat;
+  const int region = wg * H + h;
   const int rec = a.R * 4;  // doubles per matrix record
   const int ncolwg = C * WAVE;
 
+  if constexpr (PRO) sweep_prologue(a, draw, reinterpret_cast<double*>(lds_raw));
+
   unsigned char* tipl = lds_raw;
-  double* mats0 = reinterpret_cast<double*>(lds_raw + tip_lds_bytes(a.S, K));
-  double* tvec = reinterpret_cast<double*>(lds_raw + tip_nib_bytes(a.S, K));  // [16][4]
+  double* mats0 = reinterpret_cast<double*>(lds_raw + tip_lds_bytes(a.S, K, H));
+  double* tvec = reinterpret_cast<double*>(lds_raw + tip_nib_bytes(a.S, K, H));  // [16][4]
   if (threadIdx.x < 64) {  // published by the block loop's first barrier
     const unsigned b = threadIdx.x >> 2, j = threadIdx.x & 3;
     const unsigned m = b < 4 ? (1u << b) : (unsigned)(a.extra >> (4 * (b - 4))) & 15u;
@@ -507,8 +737,8 @@ __global__ void __launch_bounds__(MAXT) __attribute__((amdgpu_waves_per_eu(K == 
   const double ps_c = mdl[10 + C + c];
   const double* pmat_c = a.pmat + ((size_t)draw * C + c) * nmat * rec;
   const size_t entry2 = (size_t)K * 2 * ncolwg;  // double2 per scratch / deep-stack entry
-  double2* scr = a.scratch + (size_t)wg * a.nslots * entry2;
-  double2* dsk = a.dstk + (size_t)wg * a.ndeep * entry2;
+  double2* scr = a.scratch + (size_t)region * a.nslots * entry2;
+  double2* dsk = a.dstk + (size_t)region * a.ndeep * entry2;
   const uint32_t scr_bytes = (uint32_t)((size_t)a.nslots * entry2 * 16);
   const uint32_t dsk_bytes = (uint32_t)((size_t)a.ndeep * entry2 * 16);
   const __amdgpu_buffer_rsrc_t srd_scr = make_rsrc(scr, scr_bytes);
@@ -542,7 +772,7 @@ __global__ void __launch_bounds__(MAXT) __attribute__((amdgpu_waves_per_eu(K == 
     d[ncolwg] = make_double2(v.z, v.w);
   };
   // this wave's LDS deep entries: ndl x K x 2 halves x 64 double2
-  double2* dlw = reinterpret_cast<double2*>(tail0 + (size_t)c * tstride);
+  double2* dlw = reinterpret_cast<double2*>(tail0 + (size_t)w * tstride);
   auto dput = [&](int e, int k, const V4& v) __attribute__((always_inline)) {
     double2* d = dlw + (size_t)(e * K + k) * 2 * WAVE + lane;
     d[0] = make_double2(v.x, v.y);
@@ -555,10 +785,10 @@ __global__ void __launch_bounds__(MAXT) __attribute__((amdgpu_waves_per_eu(K == 
   };
 
   // this wave's dL/dP slot: a plain store per (branch, entry) in the
-  // workgroup's first block, then one atomic add per later block, all from
+  // region's first block, then one atomic add per later block, all from
   // this wave only -- same-address program order, so the sums are bitwise
   // reproducible and the slot needs no zeroing
-  double* gs = a.gslot + ((size_t)wg * C + c) * nmat * 16;
+  double* gs = a.gslot + ((size_t)region * C + c) * nmat * 16;
   bool gfirst = true;  // wave-uniform
 
   const int e = reduce16_entry(lane);
@@ -567,36 +797,42 @@ __global__ void __launch_bounds__(MAXT) __attribute__((amdgpu_waves_per_eu(K == 
   double acc_ll = 0.0, acc_dps = 0.0;
   V4 acc_f = {0.0, 0.0, 0.0, 0.0};
 
-  // ---- this wave's chunk of matrix records in LDS (no barrier: private) ----
+  // ---- category c's chunk of matrix records in LDS: private to the wave
+  // when H = 1 (no barrier); shared by the category's H waves otherwise
+  // (each stages every H-th piece, between two barriers -- every wave runs
+  // the same program, so all of them change chunks at the same step) ----
   int cur = -1, m0 = 0;
   auto ensure_chunk = [&](const Step& st) {
     const int ch = st.ch;
-    if (ch == cur) return;  // wave-uniform
+    if (ch == cur) return;  // workgroup-uniform
+    if (H > 1) __syncthreads();  // every wave is done with the old chunk
     const int lo = st.m0, n = st.mn;
     const double2* src = reinterpret_cast<const double2*>(pmat_c + (size_t)lo * rec);
     double2* dst = reinterpret_cast<double2*>(mats);
     const int q2 = n * rec / 2;
-    for (int k0 = lane; k0 < q2; k0 += WAVE * 8) {
+    const int str = WAVE * H;
+    for (int k0 = h * WAVE + lane; k0 < q2; k0 += str * 8) {
       double2 buf[8];
 #pragma unroll
       for (int u = 0; u < 8; ++u) {
-        const int k = k0 + u * WAVE;
+        const int k = k0 + u * str;
         buf[u] = (k < q2) ? src[k] : make_double2(0.0, 0.0);
       }
 #pragma unroll
       for (int u = 0; u < 8; ++u) {
-        const int k = k0 + u * WAVE;
+        const int k = k0 + u * str;
         if (k < q2) dst[k] = buf[u];
       }
     }
     WAIT_VMCNT0();  // no staging load may look pending inside the step loops
+    if (H > 1) __syncthreads();  // the whole chunk is staged
     cur = ch;
     m0 = lo;
   };
   auto mrec = [&](int m) __attribute__((always_inline)) -> const double* { return mats + (size_t)(m - m0) * rec; };
   // record index of tip t, column k: a nibble (two lanes share a byte)
   auto tipb = [&](int t, int k) __attribute__((always_inline)) -> unsigned {
-    return (tipl[(t * K + k) * (WAVE / 2) + (lane >> 1)] >> ((lane & 1) * 4)) & 15u;
+    return (tipl[((t * H + h) * K + k) * (WAVE / 2) + (lane >> 1)] >> ((lane & 1) * 4)) & 15u;
   };
   auto look = [&](int m, unsigned b) __attribute__((always_inline)) -> V4 {  // P t of a tip: one record vector
     const double* p = mrec(m) + (b & 15u) * 4;
@@ -632,24 +868,27 @@ __global__ void __launch_bounds__(MAXT) __attribute__((amdgpu_waves_per_eu(K == 
     }
   };
 
-  for (int blk = blockIdx.x; blk < a.nblk; blk += gridDim.x) {
+  for (int base = blockIdx.x * H; base < a.nblk; base += gridDim.x * H) {
+    const int blk = base + h;  // >= nblk: a padding block (last pass only), all columns dead
 #pragma unroll
     for (int k = 0; k < K; ++k) lofs[k] = (blk * WAVE * K + k * WAVE + lane < a.P) ? lcol[k] : OOB;
-    __syncthreads();  // the previous block's tip / root-exchange reads are done
-    // stage this block's tip bytes in LDS: S rows x 64K bytes, shared by the
-    // C category-waves and by both passes (8 loads in flight per thread)
+    __syncthreads();  // the previous pass's tip / root-exchange reads are done
+    // stage the pass's tip bytes in LDS: S rows x H x 64K nibbles, shared by
+    // the C category-waves and by both passes (8 loads in flight per thread)
     {
       const uint32_t* src = reinterpret_cast<const uint32_t*>(a.tips);
       uint32_t* dst = reinterpret_cast<uint32_t*>(tipl);
       const int rowq = a.Ppad / 8;
-      constexpr int wq = WAVE * K / 8;  // words per tip row of this block
-      const int nq = a.S * wq;
+      constexpr int wq = WAVE * K / 8;  // words per tip row of one block
+      const int hwq = H * wq;           // words per tip row of the pass
+      const int nq = a.S * hwq;
       for (int k0 = threadIdx.x; k0 < nq; k0 += nthreads * 8) {
         uint32_t buf[8];
 #pragma unroll
         for (int u = 0; u < 8; ++u) {
           const int k = k0 + u * nthreads;
-          buf[u] = (k < nq) ? src[(size_t)(k / wq) * rowq + blk * wq + (k % wq)] : 0u;
+          const int t = k / hwq, col = base * wq + (k - t * hwq);  // word of tip row t
+          buf[u] = (k < nq && col < rowq) ? src[(size_t)t * rowq + col] : a.padw;
         }
 #pragma unroll
         for (int u = 0; u < 8; ++u) {
@@ -753,14 +992,14 @@ __global__ void __launch_bounds__(MAXT) __attribute__((amdgpu_waves_per_eu(K == 
 #pragma unroll
     for (int k = 0; k < K; ++k) {
       fp[k] = vdot(pi, proot[k]);  // pi . p_root,c
-      tail0[(size_t)c * tstride + k * WAVE + lane] = ps_c * fp[k];
+      tail0[(size_t)w * tstride + k * WAVE + lane] = ps_c * fp[k];
     }
     __syncthreads();
     double L[K];
 #pragma unroll
     for (int k = 0; k < K; ++k) {
       L[k] = 0.0;
-      for (int cc = 0; cc < C; ++cc) L[k] += tail0[(size_t)cc * tstride + k * WAVE + lane];
+      for (int cc = 0; cc < C; ++cc) L[k] += tail0[(size_t)(h * C + cc) * tstride + k * WAVE + lane];
     }
     __syncthreads();  // every wave has read the exchange before deep entries are rewritten
     V4 topr[K];
@@ -768,13 +1007,13 @@ __global__ void __launch_bounds__(MAXT) __attribute__((amdgpu_waves_per_eu(K == 
     for (int k = 0; k < K; ++k) {
       const int i = blk * WAVE * K + k * WAVE + lane;  // pattern of this column
       const bool live = i < a.P;  // padding columns contribute exactly nothing
-      const double w = a.weights[i];
+      const double wt = live ? a.weights[i] : 0.0;
       const double lnL = live ? log(L[k]) : 0.0;
       if (c == 0) {
-        acc_ll += w * lnL;
+        acc_ll += wt * lnL;
         if (a.site_ll != nullptr && live) a.site_ll[(size_t)draw * a.P + i] = lnL;
       }
-      const double sc = live ? w / L[k] : 0.0;
+      const double sc = live ? wt / L[k] : 0.0;
       const double s_c = sc * ps_c;
       acc_dps = fma(sc, fp[k], acc_dps);
       acc_f.x = fma(s_c, proot[k].x, acc_f.x);
@@ -973,7 +1212,7 @@ __global__ void __launch_bounds__(MAXT) __attribute__((amdgpu_waves_per_eu(K == 
   acc_f.z = wave_sum(acc_f.z);
   acc_f.w = wave_sum(acc_f.w);
   if (lane == 0) {
-    double* ss = a.sslot + ((size_t)wg * C + c) * 8;
+    double* ss = a.sslot + ((size_t)region * C + c) * 8;
     ss[0] = acc_ll;
     ss[1] = acc_dps;
     ss[2] = acc_f.x;
@@ -982,36 +1221,43 @@ __global__ void __launch_bounds__(MAXT) __attribute__((amdgpu_waves_per_eu(K == 
     ss[5] = acc_f.w;
   }
   if (a.g_direct && !(PHY_ABLATE & 4)) {
-    // One workgroup per draw: this wave's slot is the draw's dL/dP for
-    // category c.  Write the output rows (branch order) and the chain-rule
-    // inner products <G_cb, Q P_cb> (dP/dt = Q P), 16 lanes per matrix.
-    // The atomics were performed at L2 once vmcnt drains; the slot is read
-    // back with agent-scope loads (past L1, same XCD's L2).  No device fence:
-    // a release fence here would write back the whole L2 per workgroup.
+    // One workgroup per draw: the H slots of category c (regions draw*H +
+    // h', summed in h' order) are the draw's dL/dP.  Write the output rows
+    // (branch order) and the chain-rule inner products <G_cb, Q P_cb>
+    // (dP/dt = Q P), 16 lanes per matrix, the category's H waves taking
+    // every H-th group of items.  Slots are read back with agent-scope loads
+    // (past L1: atomics were performed at L2).  No device fence: a release
+    // fence here would write back the whole L2 per workgroup.
     WAIT_VMCNT0();
     // fin: the finalize runs here; its LDS (inner products [C][B], then the
-    // waves' scalar partials [C][8]) reuses the sweep's, once every wave is done
+    // waves' scalar partials [C*H][8], then qgrad's) reuses the sweep's,
+    // once every wave is done
     double* innerL = mats0;
     double* scalL = mats0 + (size_t)C * a.B;
-    if (a.fin) __syncthreads();
+    if (a.fin || H > 1) __syncthreads();
     const double* Qd = a.eig + (size_t)draw * EIG_LEN + EIG_Q;
     double* gout = a.grows + (size_t)draw * a.grows_stride;
     double* inner_d = a.inner + (size_t)draw * C * a.B;
+    const double* gs0 = a.gslot + ((size_t)draw * H * C + c) * nmat * 16;  // region draw*H, category c
+    const size_t hstr = (size_t)C * nmat * 16;                             // next region
     // k = lane (mod 64): every item of this lane has the same entry e16 =
     // (j, kk), so the Q row is loaded once
     const int e16 = lane & 15, j = e16 >> 2, kk = e16 & 3;
     const double q0 = Qd[j * 4 + 0], q1 = Qd[j * 4 + 1], q2 = Qd[j * 4 + 2], q3 = Qd[j * 4 + 3];
     const int tot = nmat * 16;  // a multiple of 16: 16-lane groups are whole
     constexpr int U = PHY_EPI_U;
-    for (int k0 = lane; k0 < tot; k0 += WAVE * U) {
+    const int ustr = WAVE * H;
+    for (int k0 = h * WAVE + lane; k0 < tot; k0 += ustr * U) {
       double g[U], qp[U];
       int bb[U];
 #pragma unroll
       for (int u = 0; u < U; ++u) {  // all loads in flight before any use
-        const int k = k0 + u * WAVE;
+        const int k = k0 + u * ustr;
         const int kc = k < tot ? k : lane;
         const int mm = kc >> 4;
-        g[u] = __hip_atomic_load(gs + kc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        g[u] = __hip_atomic_load(gs0 + kc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        for (int hh = 1; hh < H; ++hh)
+          g[u] += __hip_atomic_load(gs0 + hh * hstr + kc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         const double2* col = reinterpret_cast<const double2*>(pmat_c + (size_t)mm * rec + kk * 4);  // column kk of P
         const double2 c01 = col[0], c23 = col[1];
         qp[u] = fma(q3, c23.y, fma(q2, c23.x, fma(q1, c01.y, q0 * c01.x)));
@@ -1019,7 +1265,7 @@ __global__ void __launch_bounds__(MAXT) __attribute__((amdgpu_waves_per_eu(K == 
       }
 #pragma unroll
       for (int u = 0; u < U; ++u) {
-        const int k = k0 + u * WAVE;
+        const int k = k0 + u * ustr;
         if (k < tot) {
           double sv = g[u] * qp[u];
           sv += __shfl_xor(sv, 8, 16);
@@ -1036,15 +1282,17 @@ __global__ void __launch_bounds__(MAXT) __attribute__((amdgpu_waves_per_eu(K == 
     }
     if (a.fin) {
       if (lane == 0) {
-        scalL[c * 8 + 0] = acc_ll;
-        scalL[c * 8 + 1] = acc_dps;
-        scalL[c * 8 + 2] = acc_f.x;
-        scalL[c * 8 + 3] = acc_f.y;
-        scalL[c * 8 + 4] = acc_f.z;
-        scalL[c * 8 + 5] = acc_f.w;
+        double* sl = scalL + (size_t)w * 8;
+        sl[0] = acc_ll;
+        sl[1] = acc_dps;
+        sl[2] = acc_f.x;
+        sl[3] = acc_f.y;
+        sl[4] = acc_f.z;
+        sl[5] = acc_f.w;
       }
       __syncthreads();
-      // finalize_kernel's sums, in its order (bitwise the same results)
+      // finalize_kernel's sums, in its order (bitwise the same results: a
+      // slot total is 0 + the H region slots in order)
       const int B = a.B;
       double* out = a.out + (size_t)draw * a.outlen;
       const double* rs = mdl + 10;
@@ -1060,14 +1308,25 @@ __global__ void __launch_bounds__(MAXT) __attribute__((amdgpu_waves_per_eu(K == 
         out[1 + B + cc] = sacc;
       }
       if (threadIdx.x == 0) {
-        const double ll = scalL[0];
+        auto tot8 = [&](int cc, int jj) {
+          double t = 0.0;
+          for (int hh = 0; hh < H; ++hh) t += scalL[(size_t)(hh * C + cc) * 8 + jj];
+          return t;
+        };
+        const double ll = tot8(0, 0);
         out[0] = isfinite(ll) ? ll : -INFINITY;
-        for (int cc = 0; cc < C; ++cc) out[1 + B + C + cc] = scalL[cc * 8 + 1];
+        for (int cc = 0; cc < C; ++cc) out[1 + B + C + cc] = tot8(cc, 1);
         for (int q = 0; q < 4; ++q) {
           double t = 0.0;
-          for (int cc = 0; cc < C; ++cc) t += scalL[cc * 8 + 2 + q];
+          for (int cc = 0; cc < C; ++cc) t += tot8(cc, 2 + q);
           out[1 + B + 2 * C + q] = t;
         }
+      }
+      if (a.qfused) {  // the Q-parameter chain rule (qgrad_kernel's work, same bits)
+        double* qsh = scalL + (size_t)C * H * 8;
+        const QgArgs q{a.eig, a.model, a.blens, a.grows, a.grows_stride, a.out, a.outlen, C, B, a.kind};
+        __syncthreads();  // dL/dP rows and the root term visible to the workgroup
+        qgrad_body(q, draw, threadIdx.x, qsh);
       }
     }
   }
@@ -1088,7 +1347,10 @@ struct PmatArgs {
 };
 
 // Cyclic Jacobi eigendecomposition of a symmetric 4x4 (A overwritten).
-__device__ void jacobi4(double A[4][4], double V[4][4], double lam[4]) {
+// No FMA contraction here or in eig_record: the host (single-launch path) and
+// the device (eig_kernel) then round every operation alike -- the same bits.
+__host__ __device__ void jacobi4(double A[4][4], double V[4][4], double lam[4]) {
+#pragma clang fp contract(off)
   for (int i = 0; i < 4; ++i)
     for (int j = 0; j < 4; ++j) V[i][j] = (i == j) ? 1.0 : 0.0;
   for (int sweep = 0; sweep < 50; ++sweep) {
@@ -1133,14 +1395,14 @@ __device__ void jacobi4(double A[4][4], double V[4][4], double lam[4]) {
   for (int i = 0; i < 4; ++i) lam[i] = A[i][i];
 }
 
-// One thread per draw: normalised Q and its eigensystem.
-__global__ void __launch_bounds__(64) eig_kernel(PmatArgs a) {
-  const int draw = blockIdx.x * blockDim.x + threadIdx.x;
-  if (draw >= a.n) return;
-  const int C = a.C;
-  const double* mdl = a.model + (size_t)draw * (10 + 2 * C);
-  double* out = a.eig + (size_t)draw * EIG_LEN;
-  if (a.kind == PHY_JC69) {  // generate_script.py:765-769 (closed form; Q for dP/dt only)
+// Normalised Q and its eigensystem of one draw's model vector (the
+// EIG_LEN record: P(t) = m1 diag(exp(lam t)) m2, Q, the normaliser).  Host
+// and device share it: eig_kernel runs it one thread per draw for batched
+// device-buffer evaluations, the single-launch small-batch path on the host
+// (a 4x4 Jacobi is a serial chain: ~12 us as one GPU thread, ~1 us here).
+__host__ __device__ void eig_record(const double* mdl, int kind, double* out) {
+#pragma clang fp contract(off)
+  if (kind == PHY_JC69) {  // generate_script.py:765-769 (closed form; Q for dP/dt only)
     for (int j = 0; j < 4; ++j)
       for (int k = 0; k < 4; ++k) out[EIG_Q + j * 4 + k] = (j == k) ? -1.0 : 1.0 / 3.0;
     return;
@@ -1188,6 +1450,13 @@ __global__ void __launch_bounds__(64) eig_kernel(PmatArgs a) {
       out[EIG_M2 + j * 4 + k] = V[k][j] * sq[k];  // V^T Pi^1/2     (:876)
     }
   }
+}
+
+// One thread per draw.
+__global__ void __launch_bounds__(64) eig_kernel(PmatArgs a) {
+  const int draw = blockIdx.x * blockDim.x + threadIdx.x;
+  if (draw >= a.n) return;
+  eig_record(a.model + (size_t)draw * (10 + 2 * a.C), a.kind, a.eig + (size_t)draw * EIG_LEN);
 }
 
 // One thread per (draw, category, matrix): the matrix record in program-use
@@ -1389,150 +1658,10 @@ __global__ void __launch_bounds__(1024) finalize_kernel(FinArgs a) {
   }
 }
 
-// dlogL / d(exchangeabilities[6], freqs[4]) through the eigendecomposition:
-// the device form of models.q_param_gradients_batch (Q = V diag(lam) V^-1,
-// V = m1 = Pi^-1/2 U, V^-1 = m2 = U^T Pi^1/2, t = r_c b):
-//   H_cb = V^T G_cb V^-T,  Phi_cb[k][l] = (e^{lam_k t} - e^{lam_l t}) / (lam_k - lam_l)
-//   (t e^{lam_k t} on ties),  M = sum_cb H_cb .* Phi_cb,  W = V^-T M V^T,
-//   qw = <Q, W>,  s = the normaliser of Q (generate_script.py:862-868);
-//   rate (i,j): (f_j W_ij + f_i W_ji - f_j W_ii - f_i W_jj - 2 f_i f_j qw) / s
-//   freq m:     (sum_{j != m} R_jm (W_jm - W_jj) - qw sum_{j != m} 2 R_mj f_j) / s
-//               + the explicit root term.
-// One workgroup per draw; per-thread partial M over (c, b) (the per-draw
-// V, V^-1, lambda and 1/(lambda_k - lambda_l) in LDS, so a thread holds only
-// M, G and one row of V^T G: ~100 VGPRs instead of 200, twice the resident
-// waves), a wave reduction of the 16 partials, then the waves in order:
-// deterministic.  JC69 has no Q parameters: zeros.
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) qgrad_kernel(FinArgs a) {
-  __shared__ double sV[16], sVi[16], srinv[16], slam[4];
-  __shared__ double part[4][16];
-  const int draw = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int C = a.C, B = a.B;
-  double* out = a.out + (size_t)draw * a.outlen;
-  const int o = 1 + B + 2 * C;
-  if (a.kind == PHY_JC69) {
-    if (tid < 10) out[o + 4 + tid] = 0.0;
-    return;
-  }
-  const double* e = a.eig + (size_t)draw * EIG_LEN;
-  if (tid < 16) {
-    sV[tid] = e[EIG_M1 + tid];
-    sVi[tid] = e[EIG_M2 + tid];
-    // 1 / (lam_k - lam_l) once per draw (0 marks a tie: t e^{lam_k t} there)
-    const double lk = e[EIG_LAM + (tid >> 2)], ll = e[EIG_LAM + (tid & 3)];
-    const double d = lk - ll;
-    srinv[tid] = fabs(d) < 1e-12 * fmax(1.0, fabs(lk)) ? 0.0 : 1.0 / d;
-    if (tid < 4) slam[tid] = e[EIG_LAM + tid];
-  }
-  __syncthreads();
-  const double* mdl = a.model + (size_t)draw * (10 + 2 * C);
-  const double* bl = a.blens + (size_t)draw * B;
-  const double* rows = a.grows + (size_t)draw * a.grows_stride;
-  // a quad of lanes per (c, b): lane k forms row k of H = V^T G V^-T and
-  // accumulates row k of M (4 values); e^{lam_k t} comes from lane k
-  const int k = tid & 3;
-  double m[4] = {0.0, 0.0, 0.0, 0.0};
-  for (int idx = tid >> 2; idx < C * B; idx += (int)(blockDim.x >> 2)) {
-    const int c = idx / B, b = idx - c * B;
-    const double t = mdl[10 + c] * bl[b];
-    double G[16];
-    const double2* g2 = reinterpret_cast<const double2*>(rows + (size_t)idx * 16);
-#pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      const double2 v = g2[u];
-      G[2 * u] = v.x;
-      G[2 * u + 1] = v.y;
-    }
-    const double Ek = exp(slam[k] * t);
-    double E[4];
-    E[0] = dpp_d<0x00>(Ek);
-    E[1] = dpp_d<0x55>(Ek);
-    E[2] = dpp_d<0xAA>(Ek);
-    E[3] = dpp_d<0xFF>(Ek);
-    double T[4];  // row k of V^T G
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      double acc = 0.0;
-#pragma unroll
-      for (int i = 0; i < 4; ++i) acc = fma(sV[i * 4 + k], G[i * 4 + j], acc);
-      T[j] = acc;
-    }
-#pragma unroll
-    for (int l = 0; l < 4; ++l) {
-      double h = 0.0;  // (V^T G V^-T)[k][l]
-#pragma unroll
-      for (int j = 0; j < 4; ++j) h = fma(T[j], sVi[l * 4 + j], h);
-      const double ri = srinv[k * 4 + l];
-      const double phi = ri == 0.0 ? t * Ek : (Ek - E[l]) * ri;
-      m[l] = fma(h, phi, m[l]);
-    }
-  }
-  // sum over the wave's 16 quads (lane bits 2..5): lanes with bits 2, 3 clear
-  // end with M[k][2 b5 + b4]
-#pragma unroll
-  for (int u = 0; u < 2; ++u) {
-    swap32(m[u], m[u + 2]);
-    m[u] += m[u + 2];
-  }
-  swap16(m[0], m[1]);
-  m[0] += m[1];
-  m[0] += dpp_d<DPP_ROW_ROR8>(m[0]);
-  m[0] += dpp_d<0x124>(m[0]);  // row_ror:4 (symmetric after the ror:8 stage)
-  if ((lane & 12) == 0) part[wave][k * 4 + ((lane >> 5) & 1) * 2 + ((lane >> 4) & 1)] = m[0];
-  __syncthreads();
-  // M = the waves' partials in order; W = V^-T M V^T, one entry per thread:
-  // W[i][j] = sum_kl Vi[k][i] M[k][l] V[j][l]
-  __shared__ double sM[16], sW[16];
-  const int nw = (int)(blockDim.x >> 6);
-  if (tid < 16) {
-    double acc = part[0][tid];
-    for (int w = 1; w < nw; ++w) acc += part[w][tid];
-    sM[tid] = acc;
-  }
-  __syncthreads();
-  if (tid < 16) {
-    const int i = tid >> 2, j = tid & 3;
-    double acc = 0.0;
-    for (int k = 0; k < 4; ++k) {
-      double ml = 0.0;
-      for (int l = 0; l < 4; ++l) ml = fma(sM[k * 4 + l], sV[j * 4 + l], ml);
-      acc = fma(sVi[k * 4 + i], ml, acc);
-    }
-    sW[tid] = acc;
-  }
-  __syncthreads();
-  if (tid != 0) return;
-  double W[16];
-  for (int k = 0; k < 16; ++k) W[k] = sW[k];
-  const double* Q = e + EIG_Q;
-  const double s = e[EIG_S];
-  double qw = 0.0;
-#pragma unroll
-  for (int k = 0; k < 16; ++k) qw = fma(Q[k], W[k], qw);
-  const double f[4] = {mdl[0], mdl[1], mdl[2], mdl[3]};
-  const double* r = mdl + 4;  // AC AG AT CG CT GT
-  const int pi_[6] = {0, 0, 0, 1, 1, 2}, pj_[6] = {1, 2, 3, 2, 3, 3};
-  double Rm[16];
-#pragma unroll
-  for (int k = 0; k < 16; ++k) Rm[k] = 0.0;
-#pragma unroll
-  for (int k = 0; k < 6; ++k) {
-    const int i = pi_[k], j = pj_[k];
-    Rm[i * 4 + j] = Rm[j * 4 + i] = r[k];
-    const double dq = f[j] * W[i * 4 + j] + f[i] * W[j * 4 + i] - f[j] * W[i * 4 + i] - f[i] * W[j * 4 + j];
-    out[o + 4 + k] = (dq - 2.0 * f[i] * f[j] * qw) / s;
-  }
-#pragma unroll
-  for (int mm = 0; mm < 4; ++mm) {
-    double dq = 0.0, ds = 0.0;
-#pragma unroll
-    for (int j = 0; j < 4; ++j)
-      if (j != mm) {
-        dq += Rm[j * 4 + mm] * (W[j * 4 + mm] - W[j * 4 + j]);
-        ds += 2.0 * Rm[mm * 4 + j] * f[j];
-      }
-    out[o + 10 + mm] = (dq - ds * qw) / s + out[o + mm];
-  }
+  __shared__ double sh[QG_SHARED];
+  const QgArgs q{a.eig, a.model, a.blens, a.grows, a.grows_stride, a.out, a.outlen, a.C, a.B, a.kind};
+  qgrad_body(q, blockIdx.x, threadIdx.x, sh);
 }
 
 }  // namespace
@@ -1545,6 +1674,8 @@ struct ClassEngine;  // class_engine.inc
 void free_class_engine(ClassEngine* e);
 struct ResEngine;  // resident_engine.inc
 void free_res_engine(ResEngine* e);
+struct MultiState;  // multi_device.inc
+void free_multi(MultiState* m);
 }  // namespace
 
 struct phy_ctx {
@@ -1555,7 +1686,10 @@ struct phy_ctx {
   int wg_budget, cols_pref, wg_cap, lds_budget;
   int cu_count = 256, wg_resident = 512;  // resident workgroups of the current plan
   int K = 1;                   // columns per lane of the current plan
-  int hmax = 1;                // most pattern blocks one workgroup runs at once (slot regions per workgroup)
+  int H = 1;                   // pattern blocks one workgroup runs at once (current plan)
+  int h_pref = 0;              // 0 automatic, else a fixed H (PHY_H)
+  bool direct_pref = true;     // single-launch small batches (PHY_DIRECT=0: off)
+  bool qfuse_pref = true;      // Q-parameter chain rule inside the sweep (PHY_QFUSE=0: off)
   int cap_m = 0, nchunks = 0;  // current LDS plan
   int deep_pref = 0;           // deep stack: 0 automatic, 1 LDS, 2 global
   bool deep_lds = false;       // current plan keeps the whole deep stack in LDS
@@ -1569,6 +1703,7 @@ struct phy_ctx {
   int engine = 0, engine_pref = 0;
   ClassEngine* ce = nullptr;
   ResEngine* re = nullptr;
+  MultiState* ms = nullptr;  // a multi-device context (phy_create_multi): its shards do the work
   bool re_tried = false;       // the resident plan was built (or found not to apply)
   int compact = 0;             // output rows without the dL/dP block (phy_set_output)
   double* d_grows = nullptr;   // dL/dP rows when compact: [max_draws][16 C B]
@@ -1593,8 +1728,10 @@ struct phy_ctx {
   // small host-buffer evaluations (phy_eval with n <= PIN_DRAWS): inputs packed
   // into one pinned staging buffer and one device buffer (one H2D copy), the
   // output rows back through pinned memory (asynchronous DMA both ways)
-  double* h_in = nullptr;   // pinned [PIN_DRAWS][B + model_len]
+  double* h_in = nullptr;   // pinned [PIN_DRAWS][B + model_len + EIG_LEN]
   double* h_out = nullptr;  // pinned [PIN_DRAWS][full output row]
+  double* h_in_dev = nullptr;   // the same buffers as the device addresses them
+  double* h_out_dev = nullptr;  // (single-launch path: the kernel reads / writes them itself)
   double* d_in = nullptr;   // device [PIN_DRAWS][B + model_len]
   int pending = 0;          // draws of a phy_eval_submit not yet collected by phy_eval_wait
   double2* d_scratch = nullptr;
@@ -1625,6 +1762,7 @@ void free_ctx(phy_ctx* c) {
   for (hipEvent_t e : c->ev) (void)hipEventDestroy(e);
   free_class_engine(c->ce);
   free_res_engine(c->re);
+  free_multi(c->ms);
   if (c->stream) (void)hipStreamDestroy(c->stream);
   (void)hipSetDevice(dev_old);
   delete c;
@@ -1821,10 +1959,22 @@ int dalloc(T** p, size_t n) {
 constexpr size_t LDS_CAP = 160 * 1024;
 
 #include "resident_engine.inc"
-constexpr int PIN_DRAWS = 64;  // phy_eval batches up to this size go through pinned staging
+constexpr int PIN_DRAWS = 128;  // phy_eval batches up to this size go through pinned staging
+                                // (ADVI's elbo_samples = 100 fits: phylostan.py:47)
 constexpr int MIN_CAP = 24;  // an occupancy level is taken only if chunks stay this large
 
 int nblk_for(int P, int K) { return (P + WAVE * K - 1) / (WAVE * K); }
+// The sweep instantiation of a plan: K columns per lane, deep stack in LDS,
+// the single-launch prologue.
+const void* sweep_kernel_ptr(int K, bool dl, bool pro) {
+  if (K == 2) {
+    if (dl) return pro ? (const void*)sweep_kernel<512, 2, true, true> : (const void*)sweep_kernel<512, 2, true, false>;
+    return pro ? (const void*)sweep_kernel<512, 2, false, true> : (const void*)sweep_kernel<512, 2, false, false>;
+  }
+  if (dl) return pro ? (const void*)sweep_kernel<1024, 1, true, true> : (const void*)sweep_kernel<1024, 1, true, false>;
+  return pro ? (const void*)sweep_kernel<1024, 1, false, true> : (const void*)sweep_kernel<1024, 1, false, false>;
+}
+int alloc_wg_buffers(phy_ctx* c, long cap);
 int waves_per_simd(int K) { return K == 2 ? PHY_WPE2 : 4; }  // the kernel's register budget
 
 // Columns per lane, matrices per LDS chunk and the chunk boundaries over the
@@ -1838,16 +1988,24 @@ int plan_chunks(phy_ctx* c) {
   if (K == 2 && c->C > 8) return fail(PHY_EINVAL, "two columns per lane need C <= 8");
   if ((size_t)std::max(c->nslots, c->ndeep) * K * 2 * c->C * WAVE * 16 >= (size_t)OOB)
     return fail(PHY_EINVAL, "per-workgroup scratch region too large for 32-bit buffer offsets");
+  // H blocks per workgroup pass: automatic = all of a draw's blocks in one
+  // pass when they fit one workgroup (C*H waves <= 8 at K = 2, 16 at K = 1):
+  // the draw's blocks share one staging of each matrix chunk, and a single
+  // workgroup per draw finishes the whole evaluation (finalize, chain rule)
+  const int hmax_wg = (K == 2 ? 8 : 16) / c->C;
+  const int nb = nblk_for(c->P, K);
+  int H = c->h_pref > 0 ? std::min(c->h_pref, hmax_wg) : (nb >= 2 && nb <= hmax_wg ? nb : 1);
+  H = std::max(1, std::min(H, nb));
   int ndl = 0;  // deep-stack entries held in LDS
   auto cap_for = [&](size_t budget) {
     int cap = c->nmat;
-    while (cap > 3 && lds_bytes(c->S, c->C, c->R, cap, K, ndl) > budget) --cap;
+    while (cap > 3 && lds_bytes(c->S, c->C, c->R, cap, K, ndl, H) > budget) --cap;
     return cap;
   };
   auto fits = [&](int cap, size_t budget) {
-    return lds_bytes(c->S, c->C, c->R, cap, K, ndl) <= budget && cap >= std::min(c->nmat, MIN_CAP);
+    return lds_bytes(c->S, c->C, c->R, cap, K, ndl, H) <= budget && cap >= std::min(c->nmat, MIN_CAP);
   };
-  const int by_waves = std::max(1, 4 * waves_per_simd(K) / c->C);  // workgroups per CU
+  const int by_waves = std::max(1, 4 * waves_per_simd(K) / (c->C * H));  // workgroups per CU
   int cap = 0;
   // Deep-stack placement at a given LDS share: the whole stack in LDS if it
   // fits beside chunks of MIN_CAP matrices (mode 0/1), else (mode 0/2) its
@@ -1876,11 +2034,25 @@ int plan_chunks(phy_ctx* c) {
     for (int t = by_waves; t >= 1; --t)
       if (place(LDS_CAP / t, t == 1)) break;
   }
-  const size_t lds = lds_bytes(c->S, c->C, c->R, cap, K, ndl);
+  const size_t lds = lds_bytes(c->S, c->C, c->R, cap, K, ndl, H);
   if (lds > LDS_CAP) return fail(PHY_EINVAL, "tree too large for LDS (tips of one block)");
   c->K = K;
-  c->nblk = nblk_for(c->P, K);
+  c->H = H;
+  c->nblk = nb;
   c->wg_resident = c->cu_count * std::min<int>(by_waves, (int)(LDS_CAP / lds));
+  {
+    // regions the largest launch of this plan may use (launch_pattern: gx
+    // workgroups per draw, H regions each), grown here so no launch fails
+    const long budget = c->wg_budget > 0 ? c->wg_budget : c->wg_resident;
+    const long per_draw = (nb + H - 1) / H;
+    const long need = (long)H * std::min<long>((long)c->max_draws * per_draw, budget + c->max_draws);
+    if (need > c->wg_cap) {
+      HIP_TRY(hipStreamSynchronize(c->stream));
+      int rc = alloc_wg_buffers(c, need);
+      if (rc) return rc;
+      c->wg_cap = (int)need;
+    }
+  }
   // chunk boundaries: matrices are numbered in step order, so a chunk is a
   // run of steps whose matrices fit
   int used = 0, ch = 0, lo = 0;
@@ -2085,8 +2257,16 @@ int launch_class(phy_ctx* ctx, int n, const double* d_blens, const double* d_mod
   return PHY_OK;
 }
 
+// Inputs of a single-launch evaluation (launch_direct): host-visible
+// (pinned) buffers the sweep's prologue reads itself.
+struct DirectIn {
+  const double* blens;  // [n][B]
+  const double* model;  // [n][10+2C]
+  const double* eig;    // [n][EIG_LEN] (eig_record on the host)
+};
 int launch_pattern(phy_ctx* ctx, int n, const double* d_blens, const double* d_model, double* d_out,
-                   double* d_site, hipStream_t st, double* grows, long long gstride);
+                   double* d_site, hipStream_t st, double* grows, long long gstride, const DirectIn* din = nullptr,
+                   bool* qdone = nullptr);
 
 void launch_finalize(const FinArgs& fa, int n, hipStream_t st) {
   const int threads = fa.gx > 64 ? 1024 : 256;
@@ -2137,56 +2317,106 @@ int launch(phy_ctx* ctx, int n, const double* d_blens, const double* d_model, do
   }
   double* grows = ctx->compact ? ctx->d_grows : d_out + PHY_OUT_G(B, C);
   const long long gstride = ctx->compact ? (long long)16 * C * B : (long long)phy_output_len(ctx);
+  bool qdone = false;
   int rc0 = ctx->engine == 1   ? launch_class(ctx, n, d_blens, d_model, d_out, d_site, st, grows, gstride)
             : ctx->engine == 2 ? launch_res(ctx, n, d_blens, d_model, d_out, d_site, st, grows, gstride)
-                               : launch_pattern(ctx, n, d_blens, d_model, d_out, d_site, st, grows, gstride);
+                               : launch_pattern(ctx, n, d_blens, d_model, d_out, d_site, st, grows, gstride,
+                                                nullptr, &qdone);
   if (rc0) return rc0;
-  FinArgs qa{ctx->d_gslot, ctx->d_sslot, ctx->d_pmat, ctx->d_eig, d_blens, d_model, ctx->d_gpos, ctx->d_inner, d_out,
-             C,            B,            ctx->nmat,   1,           phy_output_len(ctx), 0, ctx->R, grows, gstride,
-             ctx->kind};
-  hipLaunchKernelGGL(qgrad_kernel, dim3(n), dim3(256), 0, st, qa);
-  HIP_TRY(hipGetLastError());
+  if (!qdone) {
+    FinArgs qa{ctx->d_gslot, ctx->d_sslot, ctx->d_pmat, ctx->d_eig, d_blens, d_model, ctx->d_gpos, ctx->d_inner,
+               d_out,        C,            B,           ctx->nmat,   1,       phy_output_len(ctx), 0, ctx->R, grows,
+               gstride,      ctx->kind};
+    hipLaunchKernelGGL(qgrad_kernel, dim3(n), dim3(QG_THREADS), 0, st, qa);
+    HIP_TRY(hipGetLastError());
+  }
   return PHY_OK;
 }
 
-// The pattern sweep (sweep_kernel) and its dL/dP sums / finalize.
+// Can n draws run as ONE kernel launch (launch_direct)?  The pattern sweep
+// with one workgroup per draw that also runs the finalize and the chain rule.
+bool direct_ok(const phy_ctx* ctx, int n) {
+  if (!ctx->direct_pref || ctx->engine != 0 || n > PIN_DRAWS || !ctx->qfuse_pref || !ctx->fin_pref) return false;
+  const int budget = ctx->wg_budget > 0 ? ctx->wg_budget : ctx->wg_resident;
+  const int gx = std::max(1, std::min((ctx->nblk + ctx->H - 1) / ctx->H, (budget + n - 1) / n));
+  if (gx != 1) return false;
+  const size_t lds = lds_bytes(ctx->S, ctx->C, ctx->R, ctx->cap_m, ctx->K, ctx->ndl, ctx->H);
+  return ((size_t)ctx->C * ctx->B + 8 * ctx->C * ctx->H + QG_SHARED) * 8 <= lds - tip_lds_bytes(ctx->S, ctx->K, ctx->H);
+}
+
+// The single-launch small batch: host eigensystems (eig_record) go with the
+// inputs into the pinned staging; one sweep launch copies them in, builds the
+// matrix records, sweeps, finalizes, applies the chain rule and writes the
+// output rows straight into the pinned h_out (no copies, no other kernels).
+int launch_direct(phy_ctx* ctx, int n, const double* blens, const double* model, double* d_site, hipStream_t st) {
+  const int C = ctx->C, B = ctx->B, ml = 10 + 2 * C;
+  double* hb = ctx->h_in;
+  double* hm = hb + (size_t)n * B;
+  double* he = hm + (size_t)n * ml;
+  std::memcpy(hb, blens, sizeof(double) * n * B);
+  std::memcpy(hm, model, sizeof(double) * n * ml);
+  for (int d = 0; d < n; ++d) eig_record(hm + (size_t)d * ml, ctx->kind, he + (size_t)d * EIG_LEN);
+  double* db = ctx->h_in_dev;  // the device's view of the same staging
+  const DirectIn din{db, db + (size_t)n * B, db + (size_t)n * (B + ml)};
+  double* grows = ctx->compact ? ctx->d_grows : ctx->h_out_dev + PHY_OUT_G(B, C);
+  const long long gstride = ctx->compact ? (long long)16 * C * B : (long long)phy_output_len(ctx);
+  bool qdone = false;
+  int rc = launch_pattern(ctx, n, ctx->d_blens, ctx->d_model, ctx->h_out_dev, d_site, st, grows, gstride, &din,
+                          &qdone);
+  if (rc) return rc;
+  if (!qdone) return fail(PHY_EINVAL, "internal: single-launch plan without the fused chain rule");
+  return PHY_OK;
+}
+
+// The pattern sweep (sweep_kernel) and its dL/dP sums / finalize.  gx
+// workgroups per draw, each running H pattern blocks per pass (H regions).
 int launch_pattern(phy_ctx* ctx, int n, const double* d_blens, const double* d_model, double* d_out,
-                   double* d_site, hipStream_t st, double* grows, long long gstride) {
-  const int C = ctx->C, B = ctx->B;
+                   double* d_site, hipStream_t st, double* grows, long long gstride, const DirectIn* din,
+                   bool* qdone) {
+  const int C = ctx->C, B = ctx->B, H = ctx->H;
   // persistent workgroups: the explicit budget, else exactly what is resident
   const int budget = ctx->wg_budget > 0 ? ctx->wg_budget : ctx->wg_resident;
-  const int gx = std::max(1, std::min(ctx->nblk, (budget + n - 1) / n));
-  if ((size_t)gx * n > (size_t)ctx->wg_cap) return fail(PHY_ERANGE, "workgroup cap exceeded");
-  const size_t lds = lds_bytes(ctx->S, C, ctx->R, ctx->cap_m, ctx->K, ctx->ndl);
+  const int gx = std::max(1, std::min((ctx->nblk + H - 1) / H, (budget + n - 1) / n));
+  if ((size_t)gx * n * H > (size_t)ctx->wg_cap) return fail(PHY_ERANGE, "workgroup region cap exceeded");
+  const size_t lds = lds_bytes(ctx->S, C, ctx->R, ctx->cap_m, ctx->K, ctx->ndl, H);
   const int g_direct = (gx == 1) ? 1 : 0;
-  // finalize inside the sweep when its LDS holds [C][B] + [C][8] doubles past the tips
-  const int fin = (g_direct && ctx->fin_pref && ((size_t)C * B + 8 * C) * 8 <= lds - tip_lds_bytes(ctx->S, ctx->K))
-                      ? 1 : 0;
+  // finalize inside the sweep when its LDS holds [C][B] + [C*H][8] doubles
+  // past the tips; the chain rule too when QG_SHARED more fit
+  const size_t room = lds - tip_lds_bytes(ctx->S, ctx->K, H);
+  const int fin = (g_direct && ctx->fin_pref && ((size_t)C * B + 8 * C * H) * 8 <= room) ? 1 : 0;
+  const int qf = (fin && ctx->qfuse_pref && ((size_t)C * B + 8 * C * H + QG_SHARED) * 8 <= room) ? 1 : 0;
+  if (din && !qf) return fail(PHY_EINVAL, "internal: single launch needs the fused finalize and chain rule");
+  const uint32_t padn = (uint32_t)ctx->vec_of[15] & 15u;
   SweepArgs sa{ctx->d_tips,  ctx->d_w,     ctx->d_pmat,  d_model,      ctx->d_scratch, ctx->d_dstk,
                ctx->d_gslot, ctx->d_sslot, d_site,       d_out,        ctx->d_mat_branch, ctx->d_eig,
                ctx->d_inner, ctx->S,       ctx->P,       ctx->Ppad,    C,              ctx->nsteps,
                ctx->nslots,  ctx->ndeep,   ctx->ndl,     ctx->nblk,    ctx->nmat,    ctx->R,         ctx->cap_m,
-               B,            phy_output_len(ctx), g_direct, ctx->extra, fin, d_blens, grows, gstride};
+               B,            phy_output_len(ctx), g_direct, ctx->extra, fin, d_blens, grows, gstride,
+               H,            padn * 0x11111111u,  din ? 1 : 0, qf, ctx->kind,
+               din ? din->blens : nullptr, din ? din->model : nullptr, din ? din->eig : nullptr,
+               ctx->d_blens, ctx->d_model, ctx->d_eig, ctx->d_pmat};
+  if (din) {  // the prologue fills the device copies the rest of the kernel reads
+    sa.model = ctx->d_model;
+    sa.blens = ctx->d_blens;
+    sa.eig = ctx->d_eig;
+    sa.pmat = ctx->d_pmat;
+  }
   hipEvent_t e0 = nullptr, e1 = nullptr;
   if (ctx->timing) {
     int rc = timing_begin(ctx, st, &e0, &e1);
     if (rc) return rc;
   }
-  const int threads = C * WAVE;
-  if (ctx->K == 2)
-    if (ctx->deep_lds)
-      hipLaunchKernelGGL((sweep_kernel<512, 2, true>), dim3(gx, n), dim3(threads), lds, st, sa, ctx->d_prog);
-    else
-      hipLaunchKernelGGL((sweep_kernel<512, 2, false>), dim3(gx, n), dim3(threads), lds, st, sa, ctx->d_prog);
-  else
-    if (ctx->deep_lds)
-      hipLaunchKernelGGL((sweep_kernel<1024, 1, true>), dim3(gx, n), dim3(threads), lds, st, sa, ctx->d_prog);
-    else
-      hipLaunchKernelGGL((sweep_kernel<1024, 1, false>), dim3(gx, n), dim3(threads), lds, st, sa, ctx->d_prog);
+  const int threads = C * WAVE * H;
+  const void* kern = sweep_kernel_ptr(ctx->K, ctx->deep_lds, din != nullptr);
+  {
+    const int* prog = ctx->d_prog;
+    void* kargs[] = {(void*)&sa, (void*)&prog};
+    HIP_TRY(hipLaunchKernel(kern, dim3(gx, n), dim3(threads), kargs, lds, st));
+  }
   HIP_TRY(hipGetLastError());
   if (ctx->timing) HIP_TRY(hipEventRecord(e1, st));
   FinArgs fa{ctx->d_gslot, ctx->d_sslot, ctx->d_pmat, ctx->d_eig, d_blens, d_model, ctx->d_gpos, ctx->d_inner, d_out,
-             C,            B,            ctx->nmat,   gx,          phy_output_len(ctx), g_direct, ctx->R, grows, gstride,
+             C,            B,            ctx->nmat,   gx * H,      phy_output_len(ctx), g_direct, ctx->R, grows, gstride,
              ctx->kind};
   if (!g_direct) {
     hipLaunchKernelGGL(gsum_kernel, dim3((C * B * 16 + 63) / 64, n), dim3(256), 0, st, fa);
@@ -2196,10 +2426,12 @@ int launch_pattern(phy_ctx* ctx, int n, const double* d_blens, const double* d_m
     launch_finalize(fa, n, st);
     HIP_TRY(hipGetLastError());
   }
+  if (qdone) *qdone = qf != 0;
   return PHY_OK;
 }
 
-// Per-workgroup regions of the pattern sweep for `cap` workgroup slots:
+// Per-region state of the pattern sweep for `cap` regions (a region is one
+// (workgroup, h) of a launch):
 // moved-partial scratch, global deep entries, dL/dP and scalar slots.  The
 // new regions are allocated first and swapped in only when all four
 // succeed, so a failed grow leaves the context's current regions (and its
@@ -2210,8 +2442,8 @@ int alloc_wg_buffers(phy_ctx* c, long cap) {
   double *gsl = nullptr, *ssl = nullptr;
   int rc = dalloc(&scr, (size_t)cap * std::max(c->nslots, 1) * 2 * 2 * ncolwg);
   if (!rc) rc = dalloc(&dsk, (size_t)cap * std::max(c->ndeep, 1) * 2 * 2 * ncolwg);
-  if (!rc) rc = dalloc(&gsl, (size_t)cap * c->C * c->nmat * 16 * std::max(c->hmax, 1));
-  if (!rc) rc = dalloc(&ssl, (size_t)cap * c->C * 8 * std::max(c->hmax, 1));
+  if (!rc) rc = dalloc(&gsl, (size_t)cap * c->C * c->nmat * 16);
+  if (!rc) rc = dalloc(&ssl, (size_t)cap * c->C * 8);
   if (rc) {
     const std::string msg = g_err;
     void* ps[] = {scr, dsk, gsl, ssl};
@@ -2230,6 +2462,8 @@ int alloc_wg_buffers(phy_ctx* c, long cap) {
 }
 
 }  // namespace
+
+#include "multi_device.inc"
 
 extern "C" {
 
@@ -2307,6 +2541,12 @@ int phy_create(int S, int P, int C, int rooted, int model, const uint8_t* tipcod
     c->recompute = rk ? atoi(rk) != 0 : true;
     const char* fk = getenv("PHY_FIN");
     c->fin_pref = fk ? atoi(fk) != 0 : true;
+    const char* hk = getenv("PHY_H");
+    c->h_pref = hk ? std::max(0, std::min(16, atoi(hk))) : 0;
+    const char* dk2 = getenv("PHY_DIRECT");
+    c->direct_pref = dk2 ? atoi(dk2) != 0 : true;
+    const char* qk = getenv("PHY_QFUSE");
+    c->qfuse_pref = qk ? atoi(qk) != 0 : true;
 
   }
   hipError_t he = hipSetDevice(device);
@@ -2325,13 +2565,13 @@ int phy_create(int S, int P, int C, int rooted, int model, const uint8_t* tipcod
   // gfx950: one workgroup may use the whole 160 KiB LDS; dynamic LDS above
   // 64 KiB has to be opted into per kernel.
   {
-    const void* ks[] = {(const void*)sweep_kernel<1024, 1, false>, (const void*)sweep_kernel<512, 2, false>,
-                        (const void*)sweep_kernel<1024, 1, true>, (const void*)sweep_kernel<512, 2, true>};
-    for (const void* k : ks) (void)hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)LDS_CAP);
+    for (int k = 0; k < 8; ++k)
+      (void)hipFuncSetAttribute(sweep_kernel_ptr(1 + (k & 1), (k >> 1) & 1, (k >> 2) & 1),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)LDS_CAP);
     (void)hipFuncSetAttribute((const void*)res_fwd_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)LDS_CAP);
     (void)hipFuncSetAttribute((const void*)res_rev_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)LDS_CAP);
   }
-  if (lds_bytes(S, C, c->R, 3, 1, 0) > LDS_CAP) {
+  if (lds_bytes(S, C, c->R, 3, 1, 0, 1) > LDS_CAP) {
     delete c;
     return fail(PHY_EINVAL, "too many taxa for one block's tips in LDS");
   }
@@ -2372,8 +2612,10 @@ int phy_create(int S, int P, int C, int rooted, int model, const uint8_t* tipcod
     const size_t pin = (size_t)std::min(max_draws, PIN_DRAWS);
     const size_t outlen_full = (size_t)1 + c->B + 2 * C + 14 + (size_t)16 * C * c->B;
     TRY_C(dalloc(&c->d_in, pin * (c->B + 10 + 2 * C)));
-    HIP_C(hipHostMalloc((void**)&c->h_in, sizeof(double) * pin * (c->B + 10 + 2 * C), hipHostMallocDefault));
-    HIP_C(hipHostMalloc((void**)&c->h_out, sizeof(double) * pin * outlen_full, hipHostMallocDefault));
+    HIP_C(hipHostMalloc((void**)&c->h_in, sizeof(double) * pin * (c->B + 10 + 2 * C + EIG_LEN), hipHostMallocMapped));
+    HIP_C(hipHostMalloc((void**)&c->h_out, sizeof(double) * pin * outlen_full, hipHostMallocMapped));
+    HIP_C(hipHostGetDevicePointer((void**)&c->h_in_dev, c->h_in, 0));
+    HIP_C(hipHostGetDevicePointer((void**)&c->h_out_dev, c->h_out, 0));
   }
   {
     // tip nibbles: record vector of the pattern's mask (R <= 16); padding =
@@ -2425,6 +2667,80 @@ int phy_create(int S, int P, int C, int rooted, int model, const uint8_t* tipcod
   return PHY_OK;
 }
 
+int phy_create_multi(int S, int P, int C, int rooted, int model, const uint8_t* tipcodes, const double* weights,
+                     const int32_t* peel, int max_draws, int n_shards, const int* devices, phy_ctx** out) {
+  g_err.clear();
+  if (!out) return fail(PHY_EINVAL, "out is NULL");
+  *out = nullptr;
+  if (n_shards < 1 || n_shards > MAX_SHARDS) return fail(PHY_EINVAL, "n_shards must be in 1..16");
+  if (!devices || !tipcodes || !weights || !peel) return fail(PHY_EINVAL, "NULL input array");
+  if (S < 3 || P < 1) return fail(PHY_EINVAL, "need S >= 3 taxa and P >= 1 patterns");
+  bool same = true, distinct = true;
+  for (int k = 0; k < n_shards; ++k)
+    for (int j = 0; j < k; ++j) {
+      same = same && devices[j] == devices[k];
+      distinct = distinct && devices[j] != devices[k];
+    }
+  if (!same && !distinct)
+    return fail(PHY_EINVAL, "phy_create_multi: devices must be all distinct (RCCL) or all the same");
+  // contiguous ranges of whole 128-pattern blocks, counts differing by <= 1
+  const int nb = (P + 127) / 128;
+  if (n_shards > nb) return fail(PHY_EINVAL, "phy_create_multi: more shards than 128-pattern blocks");
+  MultiState* m = new MultiState();
+  m->P = P;
+  m->same_device = same;
+  {
+    int b0 = 0;
+    for (int k = 0; k < n_shards; ++k) {
+      const int nbk = nb / n_shards + (k < nb % n_shards ? 1 : 0);
+      m->p0.push_back(b0 * 128);
+      m->p1.push_back(std::min(P, (b0 + nbk) * 128));
+      b0 += nbk;
+    }
+  }
+  auto bail = [&](int rc) {
+    const std::string msg = g_err;
+    free_multi(m);
+    return fail(rc, msg);
+  };
+  for (int k = 0; k < n_shards; ++k) {
+    const int pk = m->p1[k] - m->p0[k];
+    std::vector<uint8_t> tk((size_t)S * pk);
+    for (int t = 0; t < S; ++t)
+      std::memcpy(&tk[(size_t)t * pk], tipcodes + (size_t)t * P + m->p0[k], pk);
+    phy_ctx* sh = nullptr;
+    int rc = phy_create(S, pk, C, rooted, model, tk.data(), weights + m->p0[k], peel, max_draws, devices[k], &sh);
+    if (rc) return bail(rc);
+    m->shard.push_back(sh);
+    hipEvent_t ev = nullptr;
+    if (hipSetDevice(devices[k]) != hipSuccess || hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess)
+      return bail(fail(PHY_EHIP, "hipEventCreate failed"));
+    m->ev.push_back(ev);
+  }
+  if (!same) {
+    int rc = rccl_api(&m->rccl);
+    if (rc) return bail(rc);
+    m->comm.assign(n_shards, nullptr);
+    ncclResult_t r = m->rccl->initAll(m->comm.data(), n_shards, devices);
+    if (r != ncclSuccess) {
+      m->comm.clear();
+      return bail(fail(PHY_EHIP, std::string("ncclCommInitAll: ") + m->rccl->errStr(r)));
+    }
+  }
+  phy_ctx* c = new phy_ctx();
+  c->S = S;
+  c->P = P;
+  c->C = C;
+  c->rooted = rooted ? 1 : 0;
+  c->kind = model;
+  c->max_draws = max_draws;
+  c->device = devices[0];
+  c->B = m->shard[0]->B;
+  c->ms = m;
+  *out = c;
+  return PHY_OK;
+}
+
 int phy_destroy(phy_ctx* ctx) {
   free_ctx(ctx);
   return PHY_OK;
@@ -2434,13 +2750,22 @@ int phy_num_branches(const phy_ctx* ctx) { return ctx ? ctx->B : -1; }
 
 int phy_output_len(const phy_ctx* ctx) {
   if (!ctx) return -1;
+  if (ctx->ms) return phy_output_len(ctx->ms->shard[0]);
   return PHY_OUT_G(ctx->B, ctx->C) + (ctx->compact ? 0 : 16 * ctx->C * ctx->B);
 }
 
 int phy_set_output(phy_ctx* ctx, int compact) {
   if (!ctx) return fail(PHY_EINVAL, "NULL ctx");
-  if (ctx->pending)  // phy_eval_wait copies rows of the submitted layout
+  if (ctx->pending || (ctx->ms && ctx->ms->pending))  // phy_eval_wait copies rows of the submitted layout
     return fail(PHY_EINVAL, "phy_set_output: a phy_eval_submit is still in flight (phy_eval_wait first)");
+  if (ctx->ms) {
+    for (phy_ctx* s : ctx->ms->shard) {
+      int rc = phy_set_output(s, compact);
+      if (rc) return rc;
+    }
+    ctx->compact = compact ? 1 : 0;
+    return PHY_OK;
+  }
   HIP_TRY(hipSetDevice(ctx->device));
   HIP_TRY(hipStreamSynchronize(ctx->stream));
   if (compact && !ctx->d_grows) {
@@ -2453,6 +2778,7 @@ int phy_set_output(phy_ctx* ctx, int compact) {
 
 int phy_program_info(const phy_ctx* ctx, int* nsteps, int* nslots, int* depth, int* nblocks) {
   if (!ctx) return fail(PHY_EINVAL, "NULL ctx");
+  if (ctx->ms) return phy_program_info(ctx->ms->shard[0], nsteps, nslots, depth, nblocks);
   if (nsteps) *nsteps = ctx->nsteps;
   if (nslots) *nslots = ctx->nslots;
   if (depth) *depth = ctx->ndeep;
@@ -2463,6 +2789,7 @@ int phy_program_info(const phy_ctx* ctx, int* nsteps, int* nslots, int* depth, i
 int phy_eval_device(phy_ctx* ctx, int n_draws, const double* d_blens, const double* d_model,
                     double* d_out, double* d_site_ll, void* stream) {
   if (!ctx) return fail(PHY_EINVAL, "NULL ctx");
+  if (ctx->ms) return multi_eval_device(ctx, n_draws, d_blens, d_model, d_out, d_site_ll, stream);
   if (n_draws < 1 || n_draws > ctx->max_draws) return fail(PHY_ERANGE, "n_draws out of range");
   if (!d_blens || !d_model || !d_out) return fail(PHY_EINVAL, "NULL device buffer");
   if (ctx->pending)  // the submitted evaluation still uses the context's work buffers
@@ -2477,15 +2804,30 @@ int phy_eval_device(phy_ctx* ctx, int n_draws, const double* d_blens, const doub
 // GPU work) with this evaluation.
 int phy_eval_submit(phy_ctx* ctx, int n_draws, const double* blens, const double* model) {
   if (!ctx) return fail(PHY_EINVAL, "NULL ctx");
+  if (ctx->ms) {
+    if (ctx->ms->pending) return fail(PHY_EINVAL, "phy_eval_submit: an evaluation is already in flight");
+    if (n_draws < 1 || n_draws > ctx->max_draws) return fail(PHY_ERANGE, "n_draws out of range");
+    if (!blens || !model) return fail(PHY_EINVAL, "NULL host buffer");
+    int rc = multi_enqueue(ctx, n_draws, blens, model, false);
+    if (rc) return rc;
+    ctx->ms->pending = n_draws;
+    return PHY_OK;
+  }
   if (ctx->pending) return fail(PHY_EINVAL, "phy_eval_submit: an evaluation is already in flight");
   if (n_draws < 1 || n_draws > ctx->max_draws || n_draws > PIN_DRAWS || !ctx->h_in || !ctx->h_out || !ctx->d_in)
-    return fail(PHY_ERANGE, "phy_eval_submit: n_draws must be in [1, min(max_draws, 64)]");
+    return fail(PHY_ERANGE, "phy_eval_submit: n_draws must be in [1, min(max_draws, 128)]");
   if (!blens || !model) return fail(PHY_EINVAL, "NULL host buffer");
   HIP_TRY(hipSetDevice(ctx->device));
   hipStream_t st = ctx->stream;
   const int ml = 10 + 2 * ctx->C;
   const size_t nb = (size_t)n_draws * ctx->B, nm = (size_t)n_draws * ml;
   const size_t no = (size_t)n_draws * phy_output_len(ctx);
+  if (direct_ok(ctx, n_draws)) {  // one kernel launch, rows straight into h_out
+    int rc = launch_direct(ctx, n_draws, blens, model, nullptr, st);
+    if (rc) return rc;
+    ctx->pending = n_draws;
+    return PHY_OK;
+  }
   std::memcpy(ctx->h_in, blens, sizeof(double) * nb);
   std::memcpy(ctx->h_in + nb, model, sizeof(double) * nm);
   HIP_TRY(hipMemcpyAsync(ctx->d_in, ctx->h_in, sizeof(double) * (nb + nm), hipMemcpyHostToDevice, st));
@@ -2498,6 +2840,13 @@ int phy_eval_submit(phy_ctx* ctx, int n_draws, const double* blens, const double
 
 int phy_eval_wait(phy_ctx* ctx, double* out) {
   if (!ctx) return fail(PHY_EINVAL, "NULL ctx");
+  if (ctx->ms) {
+    if (!ctx->ms->pending) return fail(PHY_EINVAL, "phy_eval_wait: nothing submitted");
+    if (!out) return fail(PHY_EINVAL, "NULL host buffer");
+    const int n = ctx->ms->pending;
+    ctx->ms->pending = 0;
+    return multi_collect(ctx, n, out, nullptr);
+  }
   if (!ctx->pending) return fail(PHY_EINVAL, "phy_eval_wait: nothing submitted");
   if (!out) return fail(PHY_EINVAL, "NULL host buffer");
   HIP_TRY(hipSetDevice(ctx->device));
@@ -2511,6 +2860,7 @@ int phy_eval_wait(phy_ctx* ctx, double* out) {
 int phy_eval(phy_ctx* ctx, int n_draws, const double* blens, const double* model, double* out,
              double* site_ll) {
   if (!ctx) return fail(PHY_EINVAL, "NULL ctx");
+  if (ctx->ms) return multi_eval(ctx, n_draws, blens, model, out, site_ll);
   if (ctx->pending) return fail(PHY_EINVAL, "phy_eval: a phy_eval_submit is still in flight (phy_eval_wait first)");
   if (n_draws < 1 || n_draws > ctx->max_draws) return fail(PHY_ERANGE, "n_draws out of range");
   if (!blens || !model || !out) return fail(PHY_EINVAL, "NULL host buffer");
@@ -2520,12 +2870,17 @@ int phy_eval(phy_ctx* ctx, int n_draws, const double* blens, const double* model
   if (n_draws <= PIN_DRAWS && ctx->h_in && ctx->h_out && ctx->d_in) {  // the small-batch (sampler) path
     const size_t nb = (size_t)n_draws * ctx->B, nm = (size_t)n_draws * ml;
     const size_t no = (size_t)n_draws * phy_output_len(ctx);
-    std::memcpy(ctx->h_in, blens, sizeof(double) * nb);
-    std::memcpy(ctx->h_in + nb, model, sizeof(double) * nm);
-    HIP_TRY(hipMemcpyAsync(ctx->d_in, ctx->h_in, sizeof(double) * (nb + nm), hipMemcpyHostToDevice, st));
-    int rc = launch(ctx, n_draws, ctx->d_in, ctx->d_in + nb, ctx->d_out, site_ll ? ctx->d_site : nullptr, st);
-    if (rc) return rc;
-    HIP_TRY(hipMemcpyAsync(ctx->h_out, ctx->d_out, sizeof(double) * no, hipMemcpyDeviceToHost, st));
+    if (direct_ok(ctx, n_draws)) {  // one kernel launch, rows straight into h_out
+      int rc = launch_direct(ctx, n_draws, blens, model, site_ll ? ctx->d_site : nullptr, st);
+      if (rc) return rc;
+    } else {
+      std::memcpy(ctx->h_in, blens, sizeof(double) * nb);
+      std::memcpy(ctx->h_in + nb, model, sizeof(double) * nm);
+      HIP_TRY(hipMemcpyAsync(ctx->d_in, ctx->h_in, sizeof(double) * (nb + nm), hipMemcpyHostToDevice, st));
+      int rc = launch(ctx, n_draws, ctx->d_in, ctx->d_in + nb, ctx->d_out, site_ll ? ctx->d_site : nullptr, st);
+      if (rc) return rc;
+      HIP_TRY(hipMemcpyAsync(ctx->h_out, ctx->d_out, sizeof(double) * no, hipMemcpyDeviceToHost, st));
+    }
     if (site_ll)
       HIP_TRY(hipMemcpyAsync(site_ll, ctx->d_site, sizeof(double) * n_draws * ctx->P, hipMemcpyDeviceToHost, st));
     HIP_TRY(hipStreamSynchronize(st));
@@ -2557,6 +2912,13 @@ double phy_pruning_loglik(phy_ctx* ctx, const double* blens, const double* model
 
 int phy_sync(phy_ctx* ctx) {
   if (!ctx) return fail(PHY_EINVAL, "NULL ctx");
+  if (ctx->ms) {
+    for (phy_ctx* s : ctx->ms->shard) {
+      int rc = phy_sync(s);
+      if (rc) return rc;
+    }
+    return PHY_OK;
+  }
   HIP_TRY(hipSetDevice(ctx->device));
   HIP_TRY(hipStreamSynchronize(ctx->stream));
   return PHY_OK;
@@ -2564,6 +2926,7 @@ int phy_sync(phy_ctx* ctx) {
 
 int phy_timing_start(phy_ctx* ctx) {
   if (!ctx) return fail(PHY_EINVAL, "NULL ctx");
+  if (ctx->ms) return phy_timing_start(ctx->ms->shard[0]);
   HIP_TRY(hipSetDevice(ctx->device));
   if (ctx->ev.empty()) {
     ctx->ev.resize(4096);
@@ -2578,6 +2941,7 @@ int phy_timing_start(phy_ctx* ctx) {
 
 int phy_timing_read(phy_ctx* ctx, double* total_ms, int* launches) {
   if (!ctx) return fail(PHY_EINVAL, "NULL ctx");
+  if (ctx->ms) return phy_timing_read(ctx->ms->shard[0], total_ms, launches);
   HIP_TRY(hipSetDevice(ctx->device));
   for (int k = 0; k + 1 < ctx->ev_used; k += 2) {
     HIP_TRY(hipEventSynchronize(ctx->ev[k + 1]));
@@ -2595,6 +2959,13 @@ int phy_timing_read(phy_ctx* ctx, double* total_ms, int* launches) {
 
 int phy_set_tuning(phy_ctx* ctx, int wg_budget, int cols, int lds_budget) {
   if (!ctx) return fail(PHY_EINVAL, "NULL ctx");
+  if (ctx->ms) {  // every shard
+    for (phy_ctx* s : ctx->ms->shard) {
+      int rc = phy_set_tuning(s, wg_budget, cols, lds_budget);
+      if (rc) return rc;
+    }
+    return PHY_OK;
+  }
   if (wg_budget > 0) {
     const long need = std::min<long>((long)nblk_for(ctx->P, 1) * ctx->max_draws,
                                      (long)std::max(wg_budget, 4 * ctx->cu_count) + ctx->max_draws);
@@ -2614,27 +2985,48 @@ int phy_set_tuning(phy_ctx* ctx, int wg_budget, int cols, int lds_budget) {
   return plan_chunks(ctx);
 }
 
-int phy_columns_per_lane(const phy_ctx* ctx) { return ctx ? ctx->K : -1; }
+int phy_columns_per_lane(const phy_ctx* ctx) { return ctx ? (ctx->ms ? ctx->ms->shard[0]->K : ctx->K) : -1; }
 
 int phy_set_deep_stack(phy_ctx* ctx, int mode) {
   if (!ctx) return fail(PHY_EINVAL, "NULL ctx");
+  if (ctx->ms) {  // every shard
+    for (phy_ctx* s : ctx->ms->shard) {
+      int rc = phy_set_deep_stack(s, mode);
+      if (rc) return rc;
+    }
+    return PHY_OK;
+  }
   if (mode < 0 || mode > 2) return fail(PHY_EINVAL, "deep-stack mode must be 0 (automatic), 1 (LDS) or 2 (global)");
   ctx->deep_pref = mode;
   HIP_TRY(hipSetDevice(ctx->device));
   return plan_chunks(ctx);
 }
-int phy_deep_stack_in_lds(const phy_ctx* ctx) { return ctx ? ctx->ndl : -1; }
+int phy_deep_stack_in_lds(const phy_ctx* ctx) { return ctx ? (ctx->ms ? ctx->ms->shard[0]->ndl : ctx->ndl) : -1; }
 
 int phy_set_recompute(phy_ctx* ctx, int on) {
   if (!ctx) return fail(PHY_EINVAL, "NULL ctx");
+  if (ctx->ms) {  // every shard
+    for (phy_ctx* s : ctx->ms->shard) {
+      int rc = phy_set_recompute(s, on);
+      if (rc) return rc;
+    }
+    return PHY_OK;
+  }
   ctx->recompute = on != 0;
   HIP_TRY(hipSetDevice(ctx->device));
   return plan_chunks(ctx);
 }
-int phy_recomputed_partials(const phy_ctx* ctx) { return ctx ? ctx->nrec : -1; }
+int phy_recomputed_partials(const phy_ctx* ctx) { return ctx ? (ctx->ms ? ctx->ms->shard[0]->nrec : ctx->nrec) : -1; }
 
 int phy_set_engine(phy_ctx* ctx, int mode) {
   if (!ctx) return fail(PHY_EINVAL, "NULL ctx");
+  if (ctx->ms) {  // every shard
+    for (phy_ctx* s : ctx->ms->shard) {
+      int rc = phy_set_engine(s, mode);
+      if (rc) return rc;
+    }
+    return PHY_OK;
+  }
   if (mode < 0 || mode > 3)
     return fail(PHY_EINVAL, "engine must be 0 (automatic), 1 (pattern), 2 (class) or 3 (resident)");
   HIP_TRY(hipSetDevice(ctx->device));
@@ -2643,11 +3035,12 @@ int phy_set_engine(phy_ctx* ctx, int mode) {
   return select_engine(ctx);
 }
 
-int phy_engine(const phy_ctx* ctx) { return ctx ? ctx->engine : -1; }
+int phy_engine(const phy_ctx* ctx) { return ctx ? (ctx->ms ? ctx->ms->shard[0]->engine : ctx->engine) : -1; }
 
 int phy_class_info(const phy_ctx* ctx, long long* classes, int* levels, int* root_classes, long long* stage,
                    long long* staged, int* tiles, int* spans) {
   if (!ctx) return fail(PHY_EINVAL, "NULL ctx");
+  if (ctx->ms) return phy_class_info(ctx->ms->shard[0], classes, levels, root_classes, stage, staged, tiles, spans);
   const ClassEngine* e = ctx->ce;
   long long ns = 0;
   int nspan = 0;
@@ -2666,6 +3059,7 @@ int phy_class_info(const phy_ctx* ctx, long long* classes, int* levels, int* roo
 
 int phy_class_clades(const phy_ctx* ctx, int* fused_levels, int* clades, long long* largest) {
   if (!ctx) return fail(PHY_EINVAL, "NULL ctx");
+  if (ctx->ms) return phy_class_clades(ctx->ms->shard[0], fused_levels, clades, largest);
   const ClassEngine* e = ctx->ce;
   if (fused_levels) *fused_levels = e ? e->Lc : 0;
   if (clades) *clades = e ? e->nclade : 0;
@@ -2676,6 +3070,7 @@ int phy_class_clades(const phy_ctx* ctx, int* fused_levels, int* clades, long lo
 int phy_resident_info(const phy_ctx* ctx, int* lds_bytes, long long* classes, int* levels, int* root_classes,
                       int* partials, int* record_vectors) {
   if (!ctx) return fail(PHY_EINVAL, "NULL ctx");
+  if (ctx->ms) return phy_resident_info(ctx->ms->shard[0], lds_bytes, classes, levels, root_classes, partials, record_vectors);
   const ResEngine* e = ctx->re;
   if (lds_bytes) *lds_bytes = e ? (int)e->lds : 0;
   if (classes) *classes = e ? e->classes : 0;
@@ -2688,10 +3083,11 @@ int phy_resident_info(const phy_ctx* ctx, int* lds_bytes, long long* classes, in
 
 int phy_lds_plan(const phy_ctx* ctx, int* n_chunks, int* matrices_per_chunk, int* lds_bytes_out) {
   if (!ctx) return fail(PHY_EINVAL, "NULL ctx");
+  if (ctx->ms) return phy_lds_plan(ctx->ms->shard[0], n_chunks, matrices_per_chunk, lds_bytes_out);
   if (n_chunks) *n_chunks = ctx->nchunks;  // matrix-record chunks per pass
   if (matrices_per_chunk) *matrices_per_chunk = ctx->cap_m;
   if (lds_bytes_out)
-    *lds_bytes_out = (int)lds_bytes(ctx->S, ctx->C, ctx->R, ctx->cap_m, ctx->K, ctx->ndl);
+    *lds_bytes_out = (int)lds_bytes(ctx->S, ctx->C, ctx->R, ctx->cap_m, ctx->K, ctx->ndl, ctx->H);
   return PHY_OK;
 }
 

@@ -64,11 +64,16 @@ class TreeLikelihood:
     C        : rate categories
     max_draws: parameter points per batched evaluation
     device   : HIP device ordinal
+    devices  : a list of device ordinals -> ONE context over len(devices)
+               contiguous pattern shards (phy_create_multi: every shard on
+               its device, one reduction of the output rows per evaluation --
+               RCCL all-reduce over distinct devices, a device-side sum when
+               they are all the same)
     """
 
     _pending = 0  # draws of a submit_rows not yet collected
 
-    def __init__(self, tipcodes, weights, peel0, rooted, model, C, max_draws=1, device=0):
+    def __init__(self, tipcodes, weights, peel0, rooted, model, C, max_draws=1, device=0, devices=None):
         self.lib = _lib.load()
         tipcodes = np.ascontiguousarray(tipcodes, dtype=np.uint8)
         self.S, self.P = tipcodes.shape
@@ -83,9 +88,15 @@ class TreeLikelihood:
         if peel.shape != (self.S - 1, 3):
             raise ValueError("peel must have shape (S-1, 3)")
         ctx = ctypes.c_void_p()
-        _lib.check(self.lib.phy_create(self.S, self.P, self.C, int(self.rooted), self.model,
-                                       _ptr(tipcodes), _ptr(w), _ptr(peel), self.max_draws,
-                                       int(device), ctypes.byref(ctx)), "phy_create")
+        if devices is not None:
+            devs = np.ascontiguousarray(devices, dtype=np.int32)
+            _lib.check(self.lib.phy_create_multi(self.S, self.P, self.C, int(self.rooted), self.model,
+                                                 _ptr(tipcodes), _ptr(w), _ptr(peel), self.max_draws,
+                                                 int(devs.size), _ptr(devs), ctypes.byref(ctx)), "phy_create_multi")
+        else:
+            _lib.check(self.lib.phy_create(self.S, self.P, self.C, int(self.rooted), self.model,
+                                           _ptr(tipcodes), _ptr(w), _ptr(peel), self.max_draws,
+                                           int(device), ctypes.byref(ctx)), "phy_create")
         self.ctx = ctx
         self.B = self.lib.phy_num_branches(ctx)
         self.outlen = self.lib.phy_output_len(ctx)
