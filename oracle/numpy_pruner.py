@@ -81,6 +81,13 @@ def model_matrices(model, freqs, qrates, blens, rs):
 
 
 def prune(tipcodes, weights, peel, rooted, pmats, freqs, ps, Q=None, blens=None, rs=None):
+    # L = 0 (a draw the sampler rejects): log L = -inf and non-finite
+    # gradients, as the GPU's -inf row -- not a numerical fault of the oracle
+    with np.errstate(divide="ignore", invalid="ignore"):
+        return _prune(tipcodes, weights, peel, rooted, pmats, freqs, ps, Q, blens, rs)
+
+
+def _prune(tipcodes, weights, peel, rooted, pmats, freqs, ps, Q=None, blens=None, rs=None):
     """Log-likelihood and gradient of one parameter point.
 
     Parameters
@@ -174,4 +181,5 @@ def loglik_only(tipcodes, weights, peel, rooted, pmats, freqs, ps):
         ay = part[y] if y == merged else np.einsum("cjk,cpk->cpj", pmats[:, y], part[y])
         part[v] = ax * ay
     L = (np.asarray(ps)[:, None] * np.einsum("j,cpj->cp", np.asarray(freqs), part[root])).sum(0)
-    return float(np.dot(weights, np.log(L))), np.log(L)
+    with np.errstate(divide="ignore"):  # L = 0: -inf, a rejected draw
+        return float(np.dot(weights, np.log(L))), np.log(L)

@@ -254,9 +254,8 @@ def run(arg, likelihood_factory=None, log=print):
     num_samples = arg.iter - num_warmup
     q0s = [post.initialize(np.random.default_rng((seed, c, 0))) for c in range(chains)]
     t0 = time.time()
-    # one batched context for all chains: pipelining two chain groups on two
-    # contexts (run_chains with a list of posteriors) measured slower here --
-    # the host's per-call cost doubles
+    # one batched context for all chains: every leapfrog round of all chains
+    # is one small-batch likelihood call
     res = run_chains(post, q0s, [(seed, c) for c in range(chains)], num_warmup=num_warmup,
                      num_samples=num_samples, thin=arg.thin, progress=log, algorithm=arg.algorithm)
     el = time.time() - t0

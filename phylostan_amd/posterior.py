@@ -502,7 +502,7 @@ class Posterior:
             pre = (vals, states, logj) if ok.all() else None  # the usual case: the constrained values are reused
             gen = self._lpg_gen(U[ok], propto, need_grad, pre)
             try:
-                with np.errstate(all="ignore"):
+                with np.errstate(over="ignore", under="ignore"):
                     req = next(gen)
             except StopIteration as e:
                 tok["done"] = e.value
@@ -512,7 +512,7 @@ class Posterior:
                 self.lik.submit_rows(*req)
                 tok["async"] = True
             else:
-                with np.errstate(all="ignore"):
+                with np.errstate(over="ignore", under="ignore"):
                     tok["rows"] = self._lik_rows(*req)
         return tok
 
@@ -524,7 +524,7 @@ class Posterior:
         if tok["gen"] is not None:
             rows = self.lik.wait_rows() if tok.get("async") else tok["rows"]
             try:
-                with np.errstate(all="ignore"):
+                with np.errstate(over="ignore", under="ignore"):
                     tok["gen"].send(rows)
                 raise RuntimeError("internal: log-density generator did not finish")
             except StopIteration as e:

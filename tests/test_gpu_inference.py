@@ -104,28 +104,6 @@ def test_fluA_nuts_short_multichain():
         assert np.all(np.isfinite(lps)) and lps[-1] > lp0[c]
 
 
-@pytest.mark.parametrize("engine", ["pattern", "resident"])
-def test_pipelined_chain_groups_equal_lockstep(engine):
-    """nuts.run_chains with two posteriors on two contexts (phy_eval_submit /
-    phy_eval_wait, one group's host work overlapping the other's evaluation)
-    gives every chain exactly the draws of the single-context lockstep run."""
-    from phylostan_amd.engine import TreeLikelihood
-    from phylostan_amd.nuts import run_chains
-    posts = []
-    for _ in range(3):
-        p, d = _fluA_posterior(TreeLikelihood, max_draws=4)
-        p.lik.set_engine(engine)
-        posts.append(p)
-    rng = np.random.default_rng(6)
-    q0s = [posts[0].initial_point(rng) for _ in range(4)]
-    one = run_chains(posts[0], q0s, [21, 22, 23, 24], num_warmup=30, num_samples=10, max_depth=6)
-    two = run_chains(posts[1:], q0s, [21, 22, 23, 24], num_warmup=30, num_samples=10, max_depth=6)
-    for a, b in zip(one, two):
-        assert a.n_grad == b.n_grad
-        for da, db in zip(a.draws, b.draws):
-            assert np.array_equal(da[0], db[0]) and da[1] == db[1]
-
-
 def test_fluA_fullrank_advi_runs_to_convergence(tmp_path):
     """-q fullrank (phylostan.py:311-313 algorithm='fullrank') with the
     reference's defaults (adapted eta, tol_rel_obj 0.001, 100000 iterations)

@@ -57,42 +57,6 @@ def test_nuts_chains_are_batched():
     assert max(tgt.batches) == 4  # one evaluation call serves every pending chain
 
 
-class GaussSplit(Gauss):
-    """The same target through log_prob_grad_begin / _end (the posterior's
-    split interface), recording the order of the calls."""
-
-    def __init__(self, mu, sd, log):
-        super().__init__(mu, sd)
-        self.log = log
-
-    def log_prob_grad_begin(self, Q):
-        self.log.append(("begin", id(self), len(Q)))
-        return np.array(Q, copy=True)
-
-    def log_prob_grad_end(self, tok):
-        self.log.append(("end", id(self), len(tok)))
-        return self.log_prob_grad(tok)
-
-
-def test_nuts_pipelined_groups_equal_lockstep():
-    """run_chains with a list of posteriors: chain i in group i mod 2, the
-    groups' evaluations interleaved (begin A, begin B, end A, begin A, end B,
-    ...), and every chain's draws exactly those of the lockstep run."""
-    mu, sd = np.array([1.0, -2.0, 0.5]), np.array([0.3, 1.0, 2.0])
-    q0s = [np.full(3, 0.2 * k) for k in range(4)]
-    one = nuts.run_chains(Gauss(mu, sd), q0s, [30 + k for k in range(4)], num_warmup=60, num_samples=40)
-    log = []
-    ga, gb = GaussSplit(mu, sd, log), GaussSplit(mu, sd, log)
-    two = nuts.run_chains([ga, gb], q0s, [30 + k for k in range(4)], num_warmup=60, num_samples=40)
-    for a, b in zip(one, two):
-        assert len(a.draws) == len(b.draws)
-        for da, db in zip(a.draws, b.draws):
-            assert np.array_equal(da[0], db[0]) and da[1] == db[1]
-    assert max(ga.batches) == 2 and max(gb.batches) == 2
-    # the second group's evaluation is started before the first group's ends
-    assert [e[0] for e in log[:3]] == ["begin", "begin", "end"]
-
-
 def test_nuts_window_schedule_matches_stan():
     ch = nuts.Chain(2, np.zeros(2), np.random.default_rng(0), num_warmup=1000)
     ends = []
@@ -233,5 +197,6 @@ def test_static_hmc_accept_no_overflow():
     """An energy drop of more than ~709 nats over one trajectory (a far-out
     start) is accepted with probability 1, not an OverflowError."""
     tgt = Gauss(np.zeros(2), np.full(2, 0.01))
-    chains = nuts.run_chains(tgt, [np.full(2, 30.0)], [7], num_warmup=30, num_samples=5, algorithm="hmc")
+    with np.errstate(over="ignore"):  # the target's own lp overflows to -inf on the far-out trajectories
+        chains = nuts.run_chains(tgt, [np.full(2, 30.0)], [7], num_warmup=30, num_samples=5, algorithm="hmc")
     assert len(chains[0].draws) == 35

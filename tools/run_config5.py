@@ -28,8 +28,6 @@ def main():
     ap.add_argument("--warmup", type=int, default=1000)
     ap.add_argument("--samples", type=int, default=1000)
     ap.add_argument("--seed", type=int, default=1)
-    ap.add_argument("--groups", type=int, default=1,
-                    help="chain groups on separate contexts, pipelined (2 measured slower: DESIGN.md 7)")
     ap.add_argument("--engine", default="latency", choices=["latency", "auto", "pattern", "resident"],
                     help="latency: the resident class sweep when it applies (what the CLI uses for NUTS)")
     ap.add_argument("--out", default=os.path.join(ROOT, "gpurun_out", "config5"))
@@ -56,10 +54,9 @@ def main():
         return Posterior(spec, tree, lik, compact_rows=True)
     post = make_post()
     lik = post.lik
-    posts = [post] + [make_post() for _ in range(a.groups - 1)]  # pipelined chain groups (nuts.run_chains)
     q0s = [post.initial_point(np.random.default_rng((a.seed, c))) for c in range(a.chains)]
     t0 = time.time()
-    chains = run_chains(posts if len(posts) > 1 else post, q0s, [(a.seed, c) for c in range(a.chains)], num_warmup=a.warmup,
+    chains = run_chains(post, q0s, [(a.seed, c) for c in range(a.chains)], num_warmup=a.warmup,
                         num_samples=a.samples, progress=lambda s: print(s, flush=True))
     el = time.time() - t0
     names = post.column_names()
@@ -85,7 +82,6 @@ def main():
     rec = {"config": "fluA HKY+W4 strict clock, constant coalescent, NUTS %d chains x (%d warmup + %d draws)"
                      % (a.chains, a.warmup, a.samples),
            "engine": lik.engine(),
-           "chain_groups": len(posts),
            "wall_s": el, "gradient_evaluations": n_grad, "grads_per_s": n_grad / el,
            "divergent": int(sum(dr[6] for ch in chains for dr in ch.draws if not dr[8])),
            "mean_accept": float(np.mean([dr[2] for ch in chains for dr in ch.draws if not dr[8]])),
