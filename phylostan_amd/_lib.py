@@ -79,7 +79,12 @@ def load(path=None):
             "(there is no CPU fallback in phylostan_amd)" % p)
     lib = ctypes.CDLL(p)
     for name, (res, args) in SIGNATURES.items():
-        fn = getattr(lib, name)
+        try:
+            fn = getattr(lib, name)
+        except AttributeError:
+            if os.environ.get("PHYLO_HIP_LIB"):  # an older variant build under A/B measurement
+                continue
+            raise PhyloHipError("%s does not export %s (stale build?)" % (p, name))
         fn.restype = res
         fn.argtypes = args
     if path is None:

@@ -492,9 +492,9 @@ __device__ __forceinline__ void build_record(const double* __restrict__ e, doubl
 // M, G and one row of V^T G: ~100 VGPRs instead of 200, twice the resident
 // waves), a wave reduction of the 16 partials, then the waves in order:
 // deterministic.  JC69 has no Q parameters: zeros.
-// qgrad_body: the work of a 256-thread workgroup (4 "virtual" waves; a
-// smaller workgroup runs them in turn, a larger one leaves its waves >= 4
-// idle), so qgrad_kernel and the sweep's fused epilogue give the same bits;
+// qgrad_body: the work of a QG_THREADS-thread workgroup (QG_THREADS / 64
+// "virtual" waves; a smaller workgroup runs them in turn), so qgrad_kernel
+// and the sweep's fused epilogue give the same bits;
 // every thread of the workgroup must call it (it holds barriers).
 // sh: QG_SHARED doubles of LDS.
 struct QgArgs {
@@ -506,16 +506,17 @@ struct QgArgs {
   double* out;          // [draw][outlen]
   int outlen, C, B, kind;
 };
-constexpr int QG_THREADS = 256;
-constexpr int QG_SHARED = 16 * 3 + 4 + 4 * 16 + 16 * 2;  // V, V^-1, 1/(lam_k - lam_l), lam, wave partials, M, W
+constexpr int QG_THREADS = 1024;  // 256 (c, b) quads per pass (the synthetic config: 1016 in 4 passes, not 16)
+constexpr int QG_SHARED = 16 * 3 + 4 + (QG_THREADS / 64) * 16 + 16 * 2;  // V, V^-1, 1/(lam_k - lam_l), lam,
+                                                                          // wave partials, M, W
 __device__ void qgrad_body(const QgArgs& a, int draw, int tid, double* sh) {
   double* sV = sh;
   double* sVi = sh + 16;
   double* srinv = sh + 32;
   double* slam = sh + 48;
-  double* part = sh + 52;  // [4][16]
-  double* sM = sh + 116;
-  double* sW = sh + 132;
+  double* part = sh + 52;  // [QG_THREADS / 64][16]
+  double* sM = part + (QG_THREADS / 64) * 16;
+  double* sW = sM + 16;
   const int lane = tid & 63, wave = tid >> 6;
   const int nwr = max(1, (int)(blockDim.x >> 6));  // the workgroup's waves
   const int C = a.C, B = a.B;
@@ -1658,7 +1659,7 @@ __global__ void __launch_bounds__(1024) finalize_kernel(FinArgs a) {
   }
 }
 
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) qgrad_kernel(FinArgs a) {
+__global__ void __launch_bounds__(QG_THREADS) qgrad_kernel(FinArgs a) {
   __shared__ double sh[QG_SHARED];
   const QgArgs q{a.eig, a.model, a.blens, a.grows, a.grows_stride, a.out, a.outlen, a.C, a.B, a.kind};
   qgrad_body(q, blockIdx.x, threadIdx.x, sh);
@@ -2216,7 +2217,7 @@ int launch_class(phy_ctx* ctx, int n, const double* d_blens, const double* d_mod
       a.count = L.ntile;
       hipLaunchKernelGGL(cls_red_kernel, dim3((L.ntile + 3) / 4, dcn), dim3(256), 0, st, a);
     }
-    if (L.nspan) {
+    if (L.nspan && !L.fixed_in_rev) {  // else summed by the REV waves of the spans' chunks
       a.first = L.span0;
       a.count = L.nspan;
       hipLaunchKernelGGL(cls_fix_kernel, dim3((L.nspan + 3) / 4, dcn), dim3(256), 0, st, a);

@@ -66,7 +66,7 @@ def main():
     from bench import kernel_source_hash
     draws = args.draws or (1 if args.workload == "synthetic" else 8192)
     bench_args = ["--workload", args.workload, "--draws", str(draws), "--steps", "3", "--warmup", "1",
-                  "--no-cpu-baseline", "--engine", args.engine]
+                  "--no-cpu-baseline", "--no-sampler-latency", "--engine", args.engine]
     tag = "%s_%s" % (args.workload, args.engine)
     fetch, nf = run_pass("FETCH_SIZE", os.path.join(args.scratch, tag + "_fetch"), bench_args, args.engine)
     write, nw = run_pass("WRITE_SIZE", os.path.join(args.scratch, tag + "_write"), bench_args, args.engine)
