@@ -138,20 +138,15 @@ int phy_eval_device(phy_ctx* ctx, int n_draws, const double* d_blens, const doub
                     double* d_out, double* d_site_ll, void* stream);
 
 /* Asynchronous small batches (host buffers, 1 <= n_draws <= min(max_draws,
- * 128)): phy_eval_submit queues the evaluation on the context's stream and
- * returns; phy_eval_wait blocks until it is done and copies the n_draws rows
- * (phy_output_len doubles each) into `out`.  When one workgroup per draw
- * runs the whole pattern sweep (the sampler-sized configs: fluA, HCV, DS1)
- * this is a SINGLE kernel launch: the inputs and their host-computed
- * eigensystems go into the context's pinned staging, which the sweep reads
- * itself; it builds the matrix records, sweeps, finalizes, applies the
- * Q-parameter chain rule and writes the rows straight into pinned memory
- * (no copies, no other kernels).  Otherwise: upload, the kernel sequence,
- * download.  One submission in flight per context (phy_eval refuses while
- * one is); contexts on one device run concurrently.  phy_eval takes the same
- * path for n_draws <= 128 (plus site log-likelihoods).  No reference
- * counterpart: the reference's log_prob is synchronous
- * (eigen/prune_stan.hpp:9-17). */
+ * 128)): phy_eval_submit copies the inputs into the context's pinned staging
+ * and queues the upload, the evaluation and the download of the output rows
+ * on the context's stream, then returns; phy_eval_wait blocks until they are
+ * done and copies the n_draws rows (phy_output_len doubles each) into `out`.
+ * One submission in flight per context (phy_eval refuses while one is);
+ * contexts on one device run concurrently.  phy_eval takes the same path for
+ * n_draws <= 128 (ADVI's elbo_samples = 100 fits), plus site
+ * log-likelihoods.  No reference counterpart: the reference's log_prob is
+ * synchronous (eigen/prune_stan.hpp:9-17). */
 int phy_eval_submit(phy_ctx* ctx, int n_draws, const double* blens, const double* model);
 int phy_eval_wait(phy_ctx* ctx, double* out);
 

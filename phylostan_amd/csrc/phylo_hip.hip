@@ -266,10 +266,10 @@ struct SweepArgs {
   const double* weights;  // [Ppad]   (0 on padding)
   const double* pmat;     // [draw][C][nmat][R][4]  matrix records, program-use order
   const double* model;    // [draw][10+2C]
-  double2* scratch;       // [region][nslots][K][2][C*64]  stored moved partials
-  double2* dstk;          // [region][ndeep][K][2][C*64]   deep-stack entries
-  double* gslot;          // [region][C][nmat][16]  dL/dP partial sums (per-wave store / atomic adds)
-  double* sslot;          // [region][C][8]
+  double2* scratch;       // [wg][nslots][K][2][C*64]  stored moved partials
+  double2* dstk;          // [wg][ndeep][K][2][C*64]   deep-stack entries
+  double* gslot;          // [wg][C][nmat][16]  dL/dP partial sums (per-wave store / atomic adds)
+  double* sslot;          // [wg][C][8]
   double* site_ll;        // [draw][P] or null
   double* out;            // [draw][outlen]: dL/dP rows written in place when g_direct
   const int* mat_branch;  // [nmat] branch of matrix m
@@ -282,49 +282,28 @@ struct SweepArgs {
   const double* blens;  // [draw][B] (fin)
   double* grows;        // dL/dP rows of draw d at grows + d * grows_stride (in `out`, or scratch when compact)
   long long grows_stride;
-  // H pattern blocks per workgroup pass: wave w = h*C + c runs category c of
-  // block h; the H waves of a category share its LDS matrix chunk.  A
-  // "region" (scratch, deep stack, dL/dP and scalar slots) belongs to one
-  // (workgroup, h): region = wg*H + h.
-  int H;
-  unsigned padw;  // eight padding nibbles (the record index of mask 15)
-  // Single-launch evaluation (pro, g_direct only): the workgroup first copies
-  // its draw's inputs from the caller's host-visible buffers (h_*) into the
-  // device buffers above (w_*) and builds the draw's matrix records
-  // (pmat_kernel's work); qfused: the Q-parameter chain rule (qgrad_kernel's
-  // work) runs after the finalize.
-  int pro, qfused, kind;
-  const double* h_blens;
-  const double* h_model;
-  const double* h_eig;
-  double* w_blens;
-  double* w_model;
-  double* w_eig;
-  double* w_pmat;
+  // qfused (fin only): the Q-parameter chain rule (qgrad_kernel's work,
+  // qgrad_body) runs after the finalize, in the same workgroup
+  int qfused, kind;
 };
 
-// LDS carve (16-B aligned pieces), K columns per lane, H blocks per pass:
-//   tips   S x H x 64K nibbles         record indices, shared by the C category waves
-//   mats   C x cap_m x R x 4 doubles  category c's chunk of matrix records
-//                                     (shared by its H waves)
+// LDS carve (16-B aligned pieces), K columns per lane:
+//   tips   S x 64K nibbles            record indices, shared by the C category waves
+//   mats   C x cap_m x R x 4 doubles  wave c's chunk of matrix records
 //   tail   per wave: ndl deep entries of K x 2 x 64 double2 (the deep
 //          entries [0, ndl) kept in LDS), or K x 64 doubles when ndl = 0;
-//          wave w's root-exchange slice (K x 64 doubles) sits at the start
+//          wave c's root-exchange slice (K x 64 doubles) sits at the start
 //          of its own tail, whose deep entries are all free at the root
-// tips: the blocks' nibbles, then the 0/1 state vectors of the 16 record
+// tips: the block's nibbles, then the 0/1 state vectors of the 16 record
 // indices (the t of dL/dP += r (x) t for a tip child: two LDS reads instead
 // of unpacking and converting its mask bits per column)
-__host__ __device__ inline size_t tip_nib_bytes(int S, int K, int H) {
-  return ((size_t)S * H * WAVE * K / 2 + 15) / 16 * 16;
-}
-__host__ __device__ inline size_t tip_lds_bytes(int S, int K, int H) {
-  return tip_nib_bytes(S, K, H) + 16 * 4 * sizeof(double);
-}
+__host__ __device__ inline size_t tip_nib_bytes(int S, int K) { return ((size_t)S * WAVE * K / 2 + 15) / 16 * 16; }
+__host__ __device__ inline size_t tip_lds_bytes(int S, int K) { return tip_nib_bytes(S, K) + 16 * 4 * sizeof(double); }
 __host__ __device__ inline size_t tail_doubles(int K, int ndl) {  // per wave
   return ndl > 0 ? (size_t)ndl * K * 2 * WAVE * 2 : (size_t)K * WAVE;
 }
-__host__ __device__ inline size_t lds_bytes(int S, int C, int R, int cap_m, int K, int ndl, int H) {
-  return tip_lds_bytes(S, K, H) + (size_t)C * cap_m * R * 32 + (size_t)C * H * tail_doubles(K, ndl) * 8;
+__host__ __device__ inline size_t lds_bytes(int S, int C, int R, int cap_m, int K, int ndl) {
+  return tip_lds_bytes(S, K) + (size_t)C * cap_m * R * 32 + (size_t)C * tail_doubles(K, ndl) * 8;
 }
 
 // Buffer resource over a workgroup's scratch / deep-stack region: loads past
@@ -648,38 +627,6 @@ __device__ void qgrad_body(const QgArgs& a, int draw, int tid, double* sh) {
   }
 }
 
-// Single-launch evaluation (SweepArgs::pro, g_direct): the workgroup copies
-// its draw's inputs from the caller's host-visible staging into LDS and the
-// device buffers, then builds the draw's matrix records (pmat_kernel's work,
-// the same build_record).  A separate instantiation of the sweep (PRO):
-// compiled into the throughput kernels it costs registers across the step
-// loops (K = 2, deep stack in LDS: 239 -> 256 VGPRs and a spill).
-__device__ __forceinline__ void sweep_prologue(const SweepArgs& a, int draw, double* inL) {
-  const int C = a.C, nmat = a.nmat, nthreads = blockDim.x, rec = a.R * 4;
-  const int B = a.B, ML = 10 + 2 * C;  // inL: [B | ML | EIG_LEN]
-  for (int k = threadIdx.x; k < B + ML + EIG_LEN; k += nthreads) {
-    double v;
-    if (k < B) {
-      v = a.h_blens[(size_t)draw * B + k];
-      a.w_blens[(size_t)draw * B + k] = v;
-    } else if (k < B + ML) {
-      v = a.h_model[(size_t)draw * ML + (k - B)];
-      a.w_model[(size_t)draw * ML + (k - B)] = v;
-    } else {
-      v = a.h_eig[(size_t)draw * EIG_LEN + (k - B - ML)];
-      a.w_eig[(size_t)draw * EIG_LEN + (k - B - ML)] = v;
-    }
-    inL[k] = v;
-  }
-  __syncthreads();
-  for (int idx = threadIdx.x; idx < C * nmat; idx += nthreads) {
-    const int cc = idx / nmat, m = idx - cc * nmat;
-    build_record(inL + B + ML, inL[a.mat_branch[m]] * inL[B + 10 + cc], a.kind, a.R, a.extra,
-                 reinterpret_cast<double2*>(a.w_pmat + ((size_t)draw * C * nmat + idx) * rec));
-  }
-  __syncthreads();  // records and inputs visible to the workgroup; LDS free again
-}
-
 // The sweep.  `prog` is a separate __restrict__ const argument so the
 // backend proves it read-only and uses scalar loads.
 //
@@ -702,27 +649,22 @@ __device__ __forceinline__ void sweep_prologue(const SweepArgs& a, int draw, dou
 #ifndef PHY_WPE2
 #define PHY_WPE2 2  // waves per SIMD the K=2 kernel is register-budgeted for
 #endif
-template <int MAXT, int K, bool DL, bool PRO>
+template <int MAXT, int K, bool DL>
 __global__ void __launch_bounds__(MAXT) __attribute__((amdgpu_waves_per_eu(K == 2 ? PHY_WPE2 : 4)))
     sweep_kernel(SweepArgs a, const int* __restrict__ prog) {
   extern __shared__ __attribute__((aligned(16))) unsigned char lds_raw[];
   const int lane = threadIdx.x & (WAVE - 1);
-  const int C = a.C, nsteps = a.nsteps, nmat = a.nmat, H = a.H;
-  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave = h * C + c
-  const int h = __builtin_amdgcn_readfirstlane(w / C);
-  const int c = w - h * C;
+  const int C = a.C, nsteps = a.nsteps, nmat = a.nmat;
+  const int c = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int nthreads = blockDim.x;
   const int draw = blockIdx.y;
   const int wg = blockIdx.y * gridDim.x + blockIdx.x;
-  const int region = wg * H + h;
   const int rec = a.R * 4;  // doubles per matrix record
   const int ncolwg = C * WAVE;
 
-  if constexpr (PRO) sweep_prologue(a, draw, reinterpret_cast<double*>(lds_raw));
-
   unsigned char* tipl = lds_raw;
-  double* mats0 = reinterpret_cast<double*>(lds_raw + tip_lds_bytes(a.S, K, H));
-  double* tvec = reinterpret_cast<double*>(lds_raw + tip_nib_bytes(a.S, K, H));  // [16][4]
+  double* mats0 = reinterpret_cast<double*>(lds_raw + tip_lds_bytes(a.S, K));
+  double* tvec = reinterpret_cast<double*>(lds_raw + tip_nib_bytes(a.S, K));  // [16][4]
   if (threadIdx.x < 64) {  // published by the block loop's first barrier
     const unsigned b = threadIdx.x >> 2, j = threadIdx.x & 3;
     const unsigned m = b < 4 ? (1u << b) : (unsigned)(a.extra >> (4 * (b - 4))) & 15u;
@@ -738,8 +680,8 @@ __global__ void __launch_bounds__(MAXT) __attribute__((amdgpu_waves_per_eu(K == 
   const double ps_c = mdl[10 + C + c];
   const double* pmat_c = a.pmat + ((size_t)draw * C + c) * nmat * rec;
   const size_t entry2 = (size_t)K * 2 * ncolwg;  // double2 per scratch / deep-stack entry
-  double2* scr = a.scratch + (size_t)region * a.nslots * entry2;
-  double2* dsk = a.dstk + (size_t)region * a.ndeep * entry2;
+  double2* scr = a.scratch + (size_t)wg * a.nslots * entry2;
+  double2* dsk = a.dstk + (size_t)wg * a.ndeep * entry2;
   const uint32_t scr_bytes = (uint32_t)((size_t)a.nslots * entry2 * 16);
   const uint32_t dsk_bytes = (uint32_t)((size_t)a.ndeep * entry2 * 16);
   const __amdgpu_buffer_rsrc_t srd_scr = make_rsrc(scr, scr_bytes);
@@ -773,7 +715,7 @@ __global__ void __launch_bounds__(MAXT) __attribute__((amdgpu_waves_per_eu(K == 
     d[ncolwg] = make_double2(v.z, v.w);
   };
   // this wave's LDS deep entries: ndl x K x 2 halves x 64 double2
-  double2* dlw = reinterpret_cast<double2*>(tail0 + (size_t)w * tstride);
+  double2* dlw = reinterpret_cast<double2*>(tail0 + (size_t)c * tstride);
   auto dput = [&](int e, int k, const V4& v) __attribute__((always_inline)) {
     double2* d = dlw + (size_t)(e * K + k) * 2 * WAVE + lane;
     d[0] = make_double2(v.x, v.y);
@@ -786,10 +728,10 @@ __global__ void __launch_bounds__(MAXT) __attribute__((amdgpu_waves_per_eu(K == 
   };
 
   // this wave's dL/dP slot: a plain store per (branch, entry) in the
-  // region's first block, then one atomic add per later block, all from
+  // workgroup's first block, then one atomic add per later block, all from
   // this wave only -- same-address program order, so the sums are bitwise
   // reproducible and the slot needs no zeroing
-  double* gs = a.gslot + ((size_t)region * C + c) * nmat * 16;
+  double* gs = a.gslot + ((size_t)wg * C + c) * nmat * 16;
   bool gfirst = true;  // wave-uniform
 
   const int e = reduce16_entry(lane);
@@ -798,42 +740,36 @@ __global__ void __launch_bounds__(MAXT) __attribute__((amdgpu_waves_per_eu(K == 
   double acc_ll = 0.0, acc_dps = 0.0;
   V4 acc_f = {0.0, 0.0, 0.0, 0.0};
 
-  // ---- category c's chunk of matrix records in LDS: private to the wave
-  // when H = 1 (no barrier); shared by the category's H waves otherwise
-  // (each stages every H-th piece, between two barriers -- every wave runs
-  // the same program, so all of them change chunks at the same step) ----
+  // ---- this wave's chunk of matrix records in LDS (no barrier: private) ----
   int cur = -1, m0 = 0;
   auto ensure_chunk = [&](const Step& st) {
     const int ch = st.ch;
-    if (ch == cur) return;  // workgroup-uniform
-    if (H > 1) __syncthreads();  // every wave is done with the old chunk
+    if (ch == cur) return;  // wave-uniform
     const int lo = st.m0, n = st.mn;
     const double2* src = reinterpret_cast<const double2*>(pmat_c + (size_t)lo * rec);
     double2* dst = reinterpret_cast<double2*>(mats);
     const int q2 = n * rec / 2;
-    const int str = WAVE * H;
-    for (int k0 = h * WAVE + lane; k0 < q2; k0 += str * 8) {
+    for (int k0 = lane; k0 < q2; k0 += WAVE * 8) {
       double2 buf[8];
 #pragma unroll
       for (int u = 0; u < 8; ++u) {
-        const int k = k0 + u * str;
+        const int k = k0 + u * WAVE;
         buf[u] = (k < q2) ? src[k] : make_double2(0.0, 0.0);
       }
 #pragma unroll
       for (int u = 0; u < 8; ++u) {
-        const int k = k0 + u * str;
+        const int k = k0 + u * WAVE;
         if (k < q2) dst[k] = buf[u];
       }
     }
     WAIT_VMCNT0();  // no staging load may look pending inside the step loops
-    if (H > 1) __syncthreads();  // the whole chunk is staged
     cur = ch;
     m0 = lo;
   };
   auto mrec = [&](int m) __attribute__((always_inline)) -> const double* { return mats + (size_t)(m - m0) * rec; };
   // record index of tip t, column k: a nibble (two lanes share a byte)
   auto tipb = [&](int t, int k) __attribute__((always_inline)) -> unsigned {
-    return (tipl[((t * H + h) * K + k) * (WAVE / 2) + (lane >> 1)] >> ((lane & 1) * 4)) & 15u;
+    return (tipl[(t * K + k) * (WAVE / 2) + (lane >> 1)] >> ((lane & 1) * 4)) & 15u;
   };
   auto look = [&](int m, unsigned b) __attribute__((always_inline)) -> V4 {  // P t of a tip: one record vector
     const double* p = mrec(m) + (b & 15u) * 4;
@@ -869,27 +805,24 @@ __global__ void __launch_bounds__(MAXT) __attribute__((amdgpu_waves_per_eu(K == 
     }
   };
 
-  for (int base = blockIdx.x * H; base < a.nblk; base += gridDim.x * H) {
-    const int blk = base + h;  // >= nblk: a padding block (last pass only), all columns dead
+  for (int blk = blockIdx.x; blk < a.nblk; blk += gridDim.x) {
 #pragma unroll
     for (int k = 0; k < K; ++k) lofs[k] = (blk * WAVE * K + k * WAVE + lane < a.P) ? lcol[k] : OOB;
-    __syncthreads();  // the previous pass's tip / root-exchange reads are done
-    // stage the pass's tip bytes in LDS: S rows x H x 64K nibbles, shared by
-    // the C category-waves and by both passes (8 loads in flight per thread)
+    __syncthreads();  // the previous block's tip / root-exchange reads are done
+    // stage this block's tip bytes in LDS: S rows x 64K bytes, shared by the
+    // C category-waves and by both passes (8 loads in flight per thread)
     {
       const uint32_t* src = reinterpret_cast<const uint32_t*>(a.tips);
       uint32_t* dst = reinterpret_cast<uint32_t*>(tipl);
       const int rowq = a.Ppad / 8;
-      constexpr int wq = WAVE * K / 8;  // words per tip row of one block
-      const int hwq = H * wq;           // words per tip row of the pass
-      const int nq = a.S * hwq;
+      constexpr int wq = WAVE * K / 8;  // words per tip row of this block
+      const int nq = a.S * wq;
       for (int k0 = threadIdx.x; k0 < nq; k0 += nthreads * 8) {
         uint32_t buf[8];
 #pragma unroll
         for (int u = 0; u < 8; ++u) {
           const int k = k0 + u * nthreads;
-          const int t = k / hwq, col = base * wq + (k - t * hwq);  // word of tip row t
-          buf[u] = (k < nq && col < rowq) ? src[(size_t)t * rowq + col] : a.padw;
+          buf[u] = (k < nq) ? src[(size_t)(k / wq) * rowq + blk * wq + (k % wq)] : 0u;
         }
 #pragma unroll
         for (int u = 0; u < 8; ++u) {
@@ -993,14 +926,14 @@ __global__ void __launch_bounds__(MAXT) __attribute__((amdgpu_waves_per_eu(K == 
 #pragma unroll
     for (int k = 0; k < K; ++k) {
       fp[k] = vdot(pi, proot[k]);  // pi . p_root,c
-      tail0[(size_t)w * tstride + k * WAVE + lane] = ps_c * fp[k];
+      tail0[(size_t)c * tstride + k * WAVE + lane] = ps_c * fp[k];
     }
     __syncthreads();
     double L[K];
 #pragma unroll
     for (int k = 0; k < K; ++k) {
       L[k] = 0.0;
-      for (int cc = 0; cc < C; ++cc) L[k] += tail0[(size_t)(h * C + cc) * tstride + k * WAVE + lane];
+      for (int cc = 0; cc < C; ++cc) L[k] += tail0[(size_t)cc * tstride + k * WAVE + lane];
     }
     __syncthreads();  // every wave has read the exchange before deep entries are rewritten
     V4 topr[K];
@@ -1008,7 +941,7 @@ __global__ void __launch_bounds__(MAXT) __attribute__((amdgpu_waves_per_eu(K == 
     for (int k = 0; k < K; ++k) {
       const int i = blk * WAVE * K + k * WAVE + lane;  // pattern of this column
       const bool live = i < a.P;  // padding columns contribute exactly nothing
-      const double wt = live ? a.weights[i] : 0.0;
+      const double wt = a.weights[i];
       const double lnL = live ? log(L[k]) : 0.0;
       if (c == 0) {
         acc_ll += wt * lnL;
@@ -1213,7 +1146,7 @@ __global__ void __launch_bounds__(MAXT) __attribute__((amdgpu_waves_per_eu(K == 
   acc_f.z = wave_sum(acc_f.z);
   acc_f.w = wave_sum(acc_f.w);
   if (lane == 0) {
-    double* ss = a.sslot + ((size_t)region * C + c) * 8;
+    double* ss = a.sslot + ((size_t)wg * C + c) * 8;
     ss[0] = acc_ll;
     ss[1] = acc_dps;
     ss[2] = acc_f.x;
@@ -1222,43 +1155,37 @@ __global__ void __launch_bounds__(MAXT) __attribute__((amdgpu_waves_per_eu(K == 
     ss[5] = acc_f.w;
   }
   if (a.g_direct && !(PHY_ABLATE & 4)) {
-    // One workgroup per draw: the H slots of category c (regions draw*H +
-    // h', summed in h' order) are the draw's dL/dP.  Write the output rows
-    // (branch order) and the chain-rule inner products <G_cb, Q P_cb>
-    // (dP/dt = Q P), 16 lanes per matrix, the category's H waves taking
-    // every H-th group of items.  Slots are read back with agent-scope loads
-    // (past L1: atomics were performed at L2).  No device fence: a release
-    // fence here would write back the whole L2 per workgroup.
+    // One workgroup per draw: this wave's slot is the draw's dL/dP for
+    // category c.  Write the output rows (branch order) and the chain-rule
+    // inner products <G_cb, Q P_cb> (dP/dt = Q P), 16 lanes per matrix.
+    // The atomics were performed at L2 once vmcnt drains; the slot is read
+    // back with agent-scope loads (past L1, same XCD's L2).  No device fence:
+    // a release fence here would write back the whole L2 per workgroup.
     WAIT_VMCNT0();
     // fin: the finalize runs here; its LDS (inner products [C][B], then the
-    // waves' scalar partials [C*H][8], then qgrad's) reuses the sweep's,
-    // once every wave is done
+    // waves' scalar partials [C][8], then qgrad's) reuses the sweep's, once
+    // every wave is done
     double* innerL = mats0;
     double* scalL = mats0 + (size_t)C * a.B;
-    if (a.fin || H > 1) __syncthreads();
+    if (a.fin) __syncthreads();
     const double* Qd = a.eig + (size_t)draw * EIG_LEN + EIG_Q;
     double* gout = a.grows + (size_t)draw * a.grows_stride;
     double* inner_d = a.inner + (size_t)draw * C * a.B;
-    const double* gs0 = a.gslot + ((size_t)draw * H * C + c) * nmat * 16;  // region draw*H, category c
-    const size_t hstr = (size_t)C * nmat * 16;                             // next region
     // k = lane (mod 64): every item of this lane has the same entry e16 =
     // (j, kk), so the Q row is loaded once
     const int e16 = lane & 15, j = e16 >> 2, kk = e16 & 3;
     const double q0 = Qd[j * 4 + 0], q1 = Qd[j * 4 + 1], q2 = Qd[j * 4 + 2], q3 = Qd[j * 4 + 3];
     const int tot = nmat * 16;  // a multiple of 16: 16-lane groups are whole
     constexpr int U = PHY_EPI_U;
-    const int ustr = WAVE * H;
-    for (int k0 = h * WAVE + lane; k0 < tot; k0 += ustr * U) {
+    for (int k0 = lane; k0 < tot; k0 += WAVE * U) {
       double g[U], qp[U];
       int bb[U];
 #pragma unroll
       for (int u = 0; u < U; ++u) {  // all loads in flight before any use
-        const int k = k0 + u * ustr;
+        const int k = k0 + u * WAVE;
         const int kc = k < tot ? k : lane;
         const int mm = kc >> 4;
-        g[u] = __hip_atomic_load(gs0 + kc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        for (int hh = 1; hh < H; ++hh)
-          g[u] += __hip_atomic_load(gs0 + hh * hstr + kc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        g[u] = __hip_atomic_load(gs + kc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         const double2* col = reinterpret_cast<const double2*>(pmat_c + (size_t)mm * rec + kk * 4);  // column kk of P
         const double2 c01 = col[0], c23 = col[1];
         qp[u] = fma(q3, c23.y, fma(q2, c23.x, fma(q1, c01.y, q0 * c01.x)));
@@ -1266,7 +1193,7 @@ __global__ void __launch_bounds__(MAXT) __attribute__((amdgpu_waves_per_eu(K == 
       }
 #pragma unroll
       for (int u = 0; u < U; ++u) {
-        const int k = k0 + u * ustr;
+        const int k = k0 + u * WAVE;
         if (k < tot) {
           double sv = g[u] * qp[u];
           sv += __shfl_xor(sv, 8, 16);
@@ -1283,7 +1210,7 @@ __global__ void __launch_bounds__(MAXT) __attribute__((amdgpu_waves_per_eu(K == 
     }
     if (a.fin) {
       if (lane == 0) {
-        double* sl = scalL + (size_t)w * 8;
+        double* sl = scalL + (size_t)c * 8;
         sl[0] = acc_ll;
         sl[1] = acc_dps;
         sl[2] = acc_f.x;
@@ -1292,8 +1219,7 @@ __global__ void __launch_bounds__(MAXT) __attribute__((amdgpu_waves_per_eu(K == 
         sl[5] = acc_f.w;
       }
       __syncthreads();
-      // finalize_kernel's sums, in its order (bitwise the same results: a
-      // slot total is 0 + the H region slots in order)
+      // finalize_kernel's sums, in its order (bitwise the same results)
       const int B = a.B;
       double* out = a.out + (size_t)draw * a.outlen;
       const double* rs = mdl + 10;
@@ -1309,11 +1235,7 @@ __global__ void __launch_bounds__(MAXT) __attribute__((amdgpu_waves_per_eu(K == 
         out[1 + B + cc] = sacc;
       }
       if (threadIdx.x == 0) {
-        auto tot8 = [&](int cc, int jj) {
-          double t = 0.0;
-          for (int hh = 0; hh < H; ++hh) t += scalL[(size_t)(hh * C + cc) * 8 + jj];
-          return t;
-        };
+        auto tot8 = [&](int cc, int jj) { return scalL[(size_t)cc * 8 + jj]; };
         const double ll = tot8(0, 0);
         out[0] = isfinite(ll) ? ll : -INFINITY;
         for (int cc = 0; cc < C; ++cc) out[1 + B + C + cc] = tot8(cc, 1);
@@ -1324,7 +1246,7 @@ __global__ void __launch_bounds__(MAXT) __attribute__((amdgpu_waves_per_eu(K == 
         }
       }
       if (a.qfused) {  // the Q-parameter chain rule (qgrad_kernel's work, same bits)
-        double* qsh = scalL + (size_t)C * H * 8;
+        double* qsh = scalL + (size_t)C * 8;
         const QgArgs q{a.eig, a.model, a.blens, a.grows, a.grows_stride, a.out, a.outlen, C, B, a.kind};
         __syncthreads();  // dL/dP rows and the root term visible to the workgroup
         qgrad_body(q, draw, threadIdx.x, qsh);
@@ -1687,9 +1609,6 @@ struct phy_ctx {
   int wg_budget, cols_pref, wg_cap, lds_budget;
   int cu_count = 256, wg_resident = 512;  // resident workgroups of the current plan
   int K = 1;                   // columns per lane of the current plan
-  int H = 1;                   // pattern blocks one workgroup runs at once (current plan)
-  int h_pref = 0;              // 0 automatic, else a fixed H (PHY_H)
-  bool direct_pref = true;     // single-launch small batches (PHY_DIRECT=0: off)
   bool qfuse_pref = true;      // Q-parameter chain rule inside the sweep (PHY_QFUSE=0: off)
   int cap_m = 0, nchunks = 0;  // current LDS plan
   int deep_pref = 0;           // deep stack: 0 automatic, 1 LDS, 2 global
@@ -1729,10 +1648,8 @@ struct phy_ctx {
   // small host-buffer evaluations (phy_eval with n <= PIN_DRAWS): inputs packed
   // into one pinned staging buffer and one device buffer (one H2D copy), the
   // output rows back through pinned memory (asynchronous DMA both ways)
-  double* h_in = nullptr;   // pinned [PIN_DRAWS][B + model_len + EIG_LEN]
+  double* h_in = nullptr;   // pinned [PIN_DRAWS][B + model_len]
   double* h_out = nullptr;  // pinned [PIN_DRAWS][full output row]
-  double* h_in_dev = nullptr;   // the same buffers as the device addresses them
-  double* h_out_dev = nullptr;  // (single-launch path: the kernel reads / writes them itself)
   double* d_in = nullptr;   // device [PIN_DRAWS][B + model_len]
   int pending = 0;          // draws of a phy_eval_submit not yet collected by phy_eval_wait
   double2* d_scratch = nullptr;
@@ -1965,15 +1882,10 @@ constexpr int PIN_DRAWS = 128;  // phy_eval batches up to this size go through p
 constexpr int MIN_CAP = 24;  // an occupancy level is taken only if chunks stay this large
 
 int nblk_for(int P, int K) { return (P + WAVE * K - 1) / (WAVE * K); }
-// The sweep instantiation of a plan: K columns per lane, deep stack in LDS,
-// the single-launch prologue.
-const void* sweep_kernel_ptr(int K, bool dl, bool pro) {
-  if (K == 2) {
-    if (dl) return pro ? (const void*)sweep_kernel<512, 2, true, true> : (const void*)sweep_kernel<512, 2, true, false>;
-    return pro ? (const void*)sweep_kernel<512, 2, false, true> : (const void*)sweep_kernel<512, 2, false, false>;
-  }
-  if (dl) return pro ? (const void*)sweep_kernel<1024, 1, true, true> : (const void*)sweep_kernel<1024, 1, true, false>;
-  return pro ? (const void*)sweep_kernel<1024, 1, false, true> : (const void*)sweep_kernel<1024, 1, false, false>;
+// The sweep instantiation of a plan: K columns per lane, deep stack in LDS.
+const void* sweep_kernel_ptr(int K, bool dl) {
+  if (K == 2) return dl ? (const void*)sweep_kernel<512, 2, true> : (const void*)sweep_kernel<512, 2, false>;
+  return dl ? (const void*)sweep_kernel<1024, 1, true> : (const void*)sweep_kernel<1024, 1, false>;
 }
 int alloc_wg_buffers(phy_ctx* c, long cap);
 int waves_per_simd(int K) { return K == 2 ? PHY_WPE2 : 4; }  // the kernel's register budget
@@ -1989,24 +1901,17 @@ int plan_chunks(phy_ctx* c) {
   if (K == 2 && c->C > 8) return fail(PHY_EINVAL, "two columns per lane need C <= 8");
   if ((size_t)std::max(c->nslots, c->ndeep) * K * 2 * c->C * WAVE * 16 >= (size_t)OOB)
     return fail(PHY_EINVAL, "per-workgroup scratch region too large for 32-bit buffer offsets");
-  // H blocks per workgroup pass: automatic = all of a draw's blocks in one
-  // pass when they fit one workgroup (C*H waves <= 8 at K = 2, 16 at K = 1):
-  // the draw's blocks share one staging of each matrix chunk, and a single
-  // workgroup per draw finishes the whole evaluation (finalize, chain rule)
-  const int hmax_wg = (K == 2 ? 8 : 16) / c->C;
   const int nb = nblk_for(c->P, K);
-  int H = c->h_pref > 0 ? std::min(c->h_pref, hmax_wg) : (nb >= 2 && nb <= hmax_wg ? nb : 1);
-  H = std::max(1, std::min(H, nb));
   int ndl = 0;  // deep-stack entries held in LDS
   auto cap_for = [&](size_t budget) {
     int cap = c->nmat;
-    while (cap > 3 && lds_bytes(c->S, c->C, c->R, cap, K, ndl, H) > budget) --cap;
+    while (cap > 3 && lds_bytes(c->S, c->C, c->R, cap, K, ndl) > budget) --cap;
     return cap;
   };
   auto fits = [&](int cap, size_t budget) {
-    return lds_bytes(c->S, c->C, c->R, cap, K, ndl, H) <= budget && cap >= std::min(c->nmat, MIN_CAP);
+    return lds_bytes(c->S, c->C, c->R, cap, K, ndl) <= budget && cap >= std::min(c->nmat, MIN_CAP);
   };
-  const int by_waves = std::max(1, 4 * waves_per_simd(K) / (c->C * H));  // workgroups per CU
+  const int by_waves = std::max(1, 4 * waves_per_simd(K) / c->C);  // workgroups per CU
   int cap = 0;
   // Deep-stack placement at a given LDS share: the whole stack in LDS if it
   // fits beside chunks of MIN_CAP matrices (mode 0/1), else (mode 0/2) its
@@ -2035,18 +1940,16 @@ int plan_chunks(phy_ctx* c) {
     for (int t = by_waves; t >= 1; --t)
       if (place(LDS_CAP / t, t == 1)) break;
   }
-  const size_t lds = lds_bytes(c->S, c->C, c->R, cap, K, ndl, H);
+  const size_t lds = lds_bytes(c->S, c->C, c->R, cap, K, ndl);
   if (lds > LDS_CAP) return fail(PHY_EINVAL, "tree too large for LDS (tips of one block)");
   c->K = K;
-  c->H = H;
   c->nblk = nb;
   c->wg_resident = c->cu_count * std::min<int>(by_waves, (int)(LDS_CAP / lds));
   {
-    // regions the largest launch of this plan may use (launch_pattern: gx
-    // workgroups per draw, H regions each), grown here so no launch fails
+    // workgroup regions the largest launch of this plan may use
+    // (launch_pattern's gx per draw), grown here so no launch fails
     const long budget = c->wg_budget > 0 ? c->wg_budget : c->wg_resident;
-    const long per_draw = (nb + H - 1) / H;
-    const long need = (long)H * std::min<long>((long)c->max_draws * per_draw, budget + c->max_draws);
+    const long need = std::min<long>((long)c->max_draws * nb, budget + c->max_draws);
     if (need > c->wg_cap) {
       HIP_TRY(hipStreamSynchronize(c->stream));
       int rc = alloc_wg_buffers(c, need);
@@ -2258,16 +2161,8 @@ int launch_class(phy_ctx* ctx, int n, const double* d_blens, const double* d_mod
   return PHY_OK;
 }
 
-// Inputs of a single-launch evaluation (launch_direct): host-visible
-// (pinned) buffers the sweep's prologue reads itself.
-struct DirectIn {
-  const double* blens;  // [n][B]
-  const double* model;  // [n][10+2C]
-  const double* eig;    // [n][EIG_LEN] (eig_record on the host)
-};
 int launch_pattern(phy_ctx* ctx, int n, const double* d_blens, const double* d_model, double* d_out,
-                   double* d_site, hipStream_t st, double* grows, long long gstride, const DirectIn* din = nullptr,
-                   bool* qdone = nullptr);
+                   double* d_site, hipStream_t st, double* grows, long long gstride, bool* qdone = nullptr);
 
 void launch_finalize(const FinArgs& fa, int n, hipStream_t st) {
   const int threads = fa.gx > 64 ? 1024 : 256;
@@ -2321,8 +2216,7 @@ int launch(phy_ctx* ctx, int n, const double* d_blens, const double* d_model, do
   bool qdone = false;
   int rc0 = ctx->engine == 1   ? launch_class(ctx, n, d_blens, d_model, d_out, d_site, st, grows, gstride)
             : ctx->engine == 2 ? launch_res(ctx, n, d_blens, d_model, d_out, d_site, st, grows, gstride)
-                               : launch_pattern(ctx, n, d_blens, d_model, d_out, d_site, st, grows, gstride,
-                                                nullptr, &qdone);
+                               : launch_pattern(ctx, n, d_blens, d_model, d_out, d_site, st, grows, gstride, &qdone);
   if (rc0) return rc0;
   if (!qdone) {
     FinArgs qa{ctx->d_gslot, ctx->d_sslot, ctx->d_pmat, ctx->d_eig, d_blens, d_model, ctx->d_gpos, ctx->d_inner,
@@ -2334,81 +2228,34 @@ int launch(phy_ctx* ctx, int n, const double* d_blens, const double* d_model, do
   return PHY_OK;
 }
 
-// Can n draws run as ONE kernel launch (launch_direct)?  The pattern sweep
-// with one workgroup per draw that also runs the finalize and the chain rule.
-bool direct_ok(const phy_ctx* ctx, int n) {
-  if (!ctx->direct_pref || ctx->engine != 0 || n > PIN_DRAWS || !ctx->qfuse_pref || !ctx->fin_pref) return false;
-  const int budget = ctx->wg_budget > 0 ? ctx->wg_budget : ctx->wg_resident;
-  const int gx = std::max(1, std::min((ctx->nblk + ctx->H - 1) / ctx->H, (budget + n - 1) / n));
-  if (gx != 1) return false;
-  const size_t lds = lds_bytes(ctx->S, ctx->C, ctx->R, ctx->cap_m, ctx->K, ctx->ndl, ctx->H);
-  return ((size_t)ctx->C * ctx->B + 8 * ctx->C * ctx->H + QG_SHARED) * 8 <= lds - tip_lds_bytes(ctx->S, ctx->K, ctx->H);
-}
-
-// The single-launch small batch: host eigensystems (eig_record) go with the
-// inputs into the pinned staging; one sweep launch copies them in, builds the
-// matrix records, sweeps, finalizes, applies the chain rule and writes the
-// output rows straight into the pinned h_out (no copies, no other kernels).
-int launch_direct(phy_ctx* ctx, int n, const double* blens, const double* model, double* d_site, hipStream_t st) {
-  const int C = ctx->C, B = ctx->B, ml = 10 + 2 * C;
-  double* hb = ctx->h_in;
-  double* hm = hb + (size_t)n * B;
-  double* he = hm + (size_t)n * ml;
-  std::memcpy(hb, blens, sizeof(double) * n * B);
-  std::memcpy(hm, model, sizeof(double) * n * ml);
-  for (int d = 0; d < n; ++d) eig_record(hm + (size_t)d * ml, ctx->kind, he + (size_t)d * EIG_LEN);
-  double* db = ctx->h_in_dev;  // the device's view of the same staging
-  const DirectIn din{db, db + (size_t)n * B, db + (size_t)n * (B + ml)};
-  double* grows = ctx->compact ? ctx->d_grows : ctx->h_out_dev + PHY_OUT_G(B, C);
-  const long long gstride = ctx->compact ? (long long)16 * C * B : (long long)phy_output_len(ctx);
-  bool qdone = false;
-  int rc = launch_pattern(ctx, n, ctx->d_blens, ctx->d_model, ctx->h_out_dev, d_site, st, grows, gstride, &din,
-                          &qdone);
-  if (rc) return rc;
-  if (!qdone) return fail(PHY_EINVAL, "internal: single-launch plan without the fused chain rule");
-  return PHY_OK;
-}
-
-// The pattern sweep (sweep_kernel) and its dL/dP sums / finalize.  gx
-// workgroups per draw, each running H pattern blocks per pass (H regions).
+// The pattern sweep (sweep_kernel) and its dL/dP sums / finalize.
 int launch_pattern(phy_ctx* ctx, int n, const double* d_blens, const double* d_model, double* d_out,
-                   double* d_site, hipStream_t st, double* grows, long long gstride, const DirectIn* din,
-                   bool* qdone) {
-  const int C = ctx->C, B = ctx->B, H = ctx->H;
+                   double* d_site, hipStream_t st, double* grows, long long gstride, bool* qdone) {
+  const int C = ctx->C, B = ctx->B;
   // persistent workgroups: the explicit budget, else exactly what is resident
   const int budget = ctx->wg_budget > 0 ? ctx->wg_budget : ctx->wg_resident;
-  const int gx = std::max(1, std::min((ctx->nblk + H - 1) / H, (budget + n - 1) / n));
-  if ((size_t)gx * n * H > (size_t)ctx->wg_cap) return fail(PHY_ERANGE, "workgroup region cap exceeded");
-  const size_t lds = lds_bytes(ctx->S, C, ctx->R, ctx->cap_m, ctx->K, ctx->ndl, H);
+  const int gx = std::max(1, std::min(ctx->nblk, (budget + n - 1) / n));
+  if ((size_t)gx * n > (size_t)ctx->wg_cap) return fail(PHY_ERANGE, "workgroup cap exceeded");
+  const size_t lds = lds_bytes(ctx->S, C, ctx->R, ctx->cap_m, ctx->K, ctx->ndl);
   const int g_direct = (gx == 1) ? 1 : 0;
-  // finalize inside the sweep when its LDS holds [C][B] + [C*H][8] doubles
+  // finalize inside the sweep when its LDS holds [C][B] + [C][8] doubles
   // past the tips; the chain rule too when QG_SHARED more fit
-  const size_t room = lds - tip_lds_bytes(ctx->S, ctx->K, H);
-  const int fin = (g_direct && ctx->fin_pref && ((size_t)C * B + 8 * C * H) * 8 <= room) ? 1 : 0;
-  const int qf = (fin && ctx->qfuse_pref && ((size_t)C * B + 8 * C * H + QG_SHARED) * 8 <= room) ? 1 : 0;
-  if (din && !qf) return fail(PHY_EINVAL, "internal: single launch needs the fused finalize and chain rule");
-  const uint32_t padn = (uint32_t)ctx->vec_of[15] & 15u;
+  const size_t room = lds - tip_lds_bytes(ctx->S, ctx->K);
+  const int fin = (g_direct && ctx->fin_pref && ((size_t)C * B + 8 * C) * 8 <= room) ? 1 : 0;
+  const int qf = (fin && ctx->qfuse_pref && ((size_t)C * B + 8 * C + QG_SHARED) * 8 <= room) ? 1 : 0;
   SweepArgs sa{ctx->d_tips,  ctx->d_w,     ctx->d_pmat,  d_model,      ctx->d_scratch, ctx->d_dstk,
                ctx->d_gslot, ctx->d_sslot, d_site,       d_out,        ctx->d_mat_branch, ctx->d_eig,
                ctx->d_inner, ctx->S,       ctx->P,       ctx->Ppad,    C,              ctx->nsteps,
                ctx->nslots,  ctx->ndeep,   ctx->ndl,     ctx->nblk,    ctx->nmat,    ctx->R,         ctx->cap_m,
                B,            phy_output_len(ctx), g_direct, ctx->extra, fin, d_blens, grows, gstride,
-               H,            padn * 0x11111111u,  din ? 1 : 0, qf, ctx->kind,
-               din ? din->blens : nullptr, din ? din->model : nullptr, din ? din->eig : nullptr,
-               ctx->d_blens, ctx->d_model, ctx->d_eig, ctx->d_pmat};
-  if (din) {  // the prologue fills the device copies the rest of the kernel reads
-    sa.model = ctx->d_model;
-    sa.blens = ctx->d_blens;
-    sa.eig = ctx->d_eig;
-    sa.pmat = ctx->d_pmat;
-  }
+               qf,           ctx->kind};
   hipEvent_t e0 = nullptr, e1 = nullptr;
   if (ctx->timing) {
     int rc = timing_begin(ctx, st, &e0, &e1);
     if (rc) return rc;
   }
-  const int threads = C * WAVE * H;
-  const void* kern = sweep_kernel_ptr(ctx->K, ctx->deep_lds, din != nullptr);
+  const int threads = C * WAVE;
+  const void* kern = sweep_kernel_ptr(ctx->K, ctx->deep_lds);
   {
     const int* prog = ctx->d_prog;
     void* kargs[] = {(void*)&sa, (void*)&prog};
@@ -2417,7 +2264,7 @@ int launch_pattern(phy_ctx* ctx, int n, const double* d_blens, const double* d_m
   HIP_TRY(hipGetLastError());
   if (ctx->timing) HIP_TRY(hipEventRecord(e1, st));
   FinArgs fa{ctx->d_gslot, ctx->d_sslot, ctx->d_pmat, ctx->d_eig, d_blens, d_model, ctx->d_gpos, ctx->d_inner, d_out,
-             C,            B,            ctx->nmat,   gx * H,      phy_output_len(ctx), g_direct, ctx->R, grows, gstride,
+             C,            B,            ctx->nmat,   gx,          phy_output_len(ctx), g_direct, ctx->R, grows, gstride,
              ctx->kind};
   if (!g_direct) {
     hipLaunchKernelGGL(gsum_kernel, dim3((C * B * 16 + 63) / 64, n), dim3(256), 0, st, fa);
@@ -2431,8 +2278,7 @@ int launch_pattern(phy_ctx* ctx, int n, const double* d_blens, const double* d_m
   return PHY_OK;
 }
 
-// Per-region state of the pattern sweep for `cap` regions (a region is one
-// (workgroup, h) of a launch):
+// Per-workgroup regions of the pattern sweep for `cap` workgroup slots:
 // moved-partial scratch, global deep entries, dL/dP and scalar slots.  The
 // new regions are allocated first and swapped in only when all four
 // succeed, so a failed grow leaves the context's current regions (and its
@@ -2542,10 +2388,6 @@ int phy_create(int S, int P, int C, int rooted, int model, const uint8_t* tipcod
     c->recompute = rk ? atoi(rk) != 0 : true;
     const char* fk = getenv("PHY_FIN");
     c->fin_pref = fk ? atoi(fk) != 0 : true;
-    const char* hk = getenv("PHY_H");
-    c->h_pref = hk ? std::max(0, std::min(16, atoi(hk))) : 0;
-    const char* dk2 = getenv("PHY_DIRECT");
-    c->direct_pref = dk2 ? atoi(dk2) != 0 : true;
     const char* qk = getenv("PHY_QFUSE");
     c->qfuse_pref = qk ? atoi(qk) != 0 : true;
 
@@ -2566,13 +2408,13 @@ int phy_create(int S, int P, int C, int rooted, int model, const uint8_t* tipcod
   // gfx950: one workgroup may use the whole 160 KiB LDS; dynamic LDS above
   // 64 KiB has to be opted into per kernel.
   {
-    for (int k = 0; k < 8; ++k)
-      (void)hipFuncSetAttribute(sweep_kernel_ptr(1 + (k & 1), (k >> 1) & 1, (k >> 2) & 1),
-                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)LDS_CAP);
+    for (int k = 0; k < 4; ++k)
+      (void)hipFuncSetAttribute(sweep_kernel_ptr(1 + (k & 1), (k >> 1) & 1), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                (int)LDS_CAP);
     (void)hipFuncSetAttribute((const void*)res_fwd_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)LDS_CAP);
     (void)hipFuncSetAttribute((const void*)res_rev_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)LDS_CAP);
   }
-  if (lds_bytes(S, C, c->R, 3, 1, 0, 1) > LDS_CAP) {
+  if (lds_bytes(S, C, c->R, 3, 1, 0) > LDS_CAP) {
     delete c;
     return fail(PHY_EINVAL, "too many taxa for one block's tips in LDS");
   }
@@ -2613,10 +2455,8 @@ int phy_create(int S, int P, int C, int rooted, int model, const uint8_t* tipcod
     const size_t pin = (size_t)std::min(max_draws, PIN_DRAWS);
     const size_t outlen_full = (size_t)1 + c->B + 2 * C + 14 + (size_t)16 * C * c->B;
     TRY_C(dalloc(&c->d_in, pin * (c->B + 10 + 2 * C)));
-    HIP_C(hipHostMalloc((void**)&c->h_in, sizeof(double) * pin * (c->B + 10 + 2 * C + EIG_LEN), hipHostMallocMapped));
-    HIP_C(hipHostMalloc((void**)&c->h_out, sizeof(double) * pin * outlen_full, hipHostMallocMapped));
-    HIP_C(hipHostGetDevicePointer((void**)&c->h_in_dev, c->h_in, 0));
-    HIP_C(hipHostGetDevicePointer((void**)&c->h_out_dev, c->h_out, 0));
+    HIP_C(hipHostMalloc((void**)&c->h_in, sizeof(double) * pin * (c->B + 10 + 2 * C), hipHostMallocDefault));
+    HIP_C(hipHostMalloc((void**)&c->h_out, sizeof(double) * pin * outlen_full, hipHostMallocDefault));
   }
   {
     // tip nibbles: record vector of the pattern's mask (R <= 16); padding =
@@ -2823,12 +2663,6 @@ int phy_eval_submit(phy_ctx* ctx, int n_draws, const double* blens, const double
   const int ml = 10 + 2 * ctx->C;
   const size_t nb = (size_t)n_draws * ctx->B, nm = (size_t)n_draws * ml;
   const size_t no = (size_t)n_draws * phy_output_len(ctx);
-  if (direct_ok(ctx, n_draws)) {  // one kernel launch, rows straight into h_out
-    int rc = launch_direct(ctx, n_draws, blens, model, nullptr, st);
-    if (rc) return rc;
-    ctx->pending = n_draws;
-    return PHY_OK;
-  }
   std::memcpy(ctx->h_in, blens, sizeof(double) * nb);
   std::memcpy(ctx->h_in + nb, model, sizeof(double) * nm);
   HIP_TRY(hipMemcpyAsync(ctx->d_in, ctx->h_in, sizeof(double) * (nb + nm), hipMemcpyHostToDevice, st));
@@ -2871,17 +2705,12 @@ int phy_eval(phy_ctx* ctx, int n_draws, const double* blens, const double* model
   if (n_draws <= PIN_DRAWS && ctx->h_in && ctx->h_out && ctx->d_in) {  // the small-batch (sampler) path
     const size_t nb = (size_t)n_draws * ctx->B, nm = (size_t)n_draws * ml;
     const size_t no = (size_t)n_draws * phy_output_len(ctx);
-    if (direct_ok(ctx, n_draws)) {  // one kernel launch, rows straight into h_out
-      int rc = launch_direct(ctx, n_draws, blens, model, site_ll ? ctx->d_site : nullptr, st);
-      if (rc) return rc;
-    } else {
-      std::memcpy(ctx->h_in, blens, sizeof(double) * nb);
-      std::memcpy(ctx->h_in + nb, model, sizeof(double) * nm);
-      HIP_TRY(hipMemcpyAsync(ctx->d_in, ctx->h_in, sizeof(double) * (nb + nm), hipMemcpyHostToDevice, st));
-      int rc = launch(ctx, n_draws, ctx->d_in, ctx->d_in + nb, ctx->d_out, site_ll ? ctx->d_site : nullptr, st);
-      if (rc) return rc;
-      HIP_TRY(hipMemcpyAsync(ctx->h_out, ctx->d_out, sizeof(double) * no, hipMemcpyDeviceToHost, st));
-    }
+    std::memcpy(ctx->h_in, blens, sizeof(double) * nb);
+    std::memcpy(ctx->h_in + nb, model, sizeof(double) * nm);
+    HIP_TRY(hipMemcpyAsync(ctx->d_in, ctx->h_in, sizeof(double) * (nb + nm), hipMemcpyHostToDevice, st));
+    int rc = launch(ctx, n_draws, ctx->d_in, ctx->d_in + nb, ctx->d_out, site_ll ? ctx->d_site : nullptr, st);
+    if (rc) return rc;
+    HIP_TRY(hipMemcpyAsync(ctx->h_out, ctx->d_out, sizeof(double) * no, hipMemcpyDeviceToHost, st));
     if (site_ll)
       HIP_TRY(hipMemcpyAsync(site_ll, ctx->d_site, sizeof(double) * n_draws * ctx->P, hipMemcpyDeviceToHost, st));
     HIP_TRY(hipStreamSynchronize(st));
@@ -3088,7 +2917,7 @@ int phy_lds_plan(const phy_ctx* ctx, int* n_chunks, int* matrices_per_chunk, int
   if (n_chunks) *n_chunks = ctx->nchunks;  // matrix-record chunks per pass
   if (matrices_per_chunk) *matrices_per_chunk = ctx->cap_m;
   if (lds_bytes_out)
-    *lds_bytes_out = (int)lds_bytes(ctx->S, ctx->C, ctx->R, ctx->cap_m, ctx->K, ctx->ndl, ctx->H);
+    *lds_bytes_out = (int)lds_bytes(ctx->S, ctx->C, ctx->R, ctx->cap_m, ctx->K, ctx->ndl);
   return PHY_OK;
 }
 

@@ -308,7 +308,6 @@ def test_finalize_inside_sweep_matches_kernel(monkeypatch):
     n = 3
     blens = base.blens[None, :] * rng.uniform(0.7, 1.3, (n, 1))
     mv = np.repeat(base.model_vec()[None], n, axis=0)
-    monkeypatch.setenv("PHY_DIRECT", "0")  # both through eig / pmat kernels + sweep (+ finalize)
     eng = _engine(base, max_draws=n)
     eng.set_tuning(n, 0, 0)  # one workgroup per draw
     r1 = eng.evaluate_batch(blens, mv, site_ll=True)
@@ -390,26 +389,3 @@ def test_tuning_grows_workgroup_regions_past_create():
     _close(got.dLdP, ref.dLdP, RTOL_G, "dLdP")
     check_case(case, eng, got)
 
-
-@pytest.mark.parametrize("make", [cases.fluA_case, cases.hcv_case, cases.ds1_case], ids=["fluA", "HCV", "DS1"])
-def test_single_launch_equals_kernel_sequence(make, monkeypatch):
-    """The small-batch single launch (host eigensystems, the sweep building
-    its matrix records, finalize and chain rule fused, rows written into the
-    pinned staging) gives the eig / pmat / sweep / finalize / qgrad
-    sequence's rows bit for bit, full and compact."""
-    base = make()
-    rng = np.random.default_rng(8)
-    n = 5
-    blens = base.blens[None, :] * rng.uniform(0.7, 1.3, (n, 1))
-    mv = np.repeat(base.model_vec()[None], n, axis=0)
-    eng = _engine(base, max_draws=n)
-    monkeypatch.setenv("PHY_DIRECT", "0")
-    ref = _engine(base, max_draws=n)
-    for compact in (False, True):
-        eng.set_output(compact=compact)
-        ref.set_output(compact=compact)
-        a = eng.evaluate_rows(blens, mv)
-        b = ref.evaluate_rows(blens, mv)
-        assert np.array_equal(a, b), np.max(np.abs(a - b))
-    eng.set_output(compact=False)
-    check_case(base, eng)
