@@ -276,10 +276,11 @@ def run(arg, likelihood_factory=None, log=print):
 
 def parse(arg):
     tree = dataio.read_tree(arg.tree)
-    # the reference reroots a multifurcating root here (phylostan.py:140-141)
-    # but resolves polytomies in run (:175); resolving here too keeps the node
-    # numbering of the sample file's run
-    tree.resolve_polytomies(update_bipartitions=True)
+    # phylostan.py:140-141: a root with more than two children is rerooted at
+    # its first child's edge (run resolves polytomies instead, :175; for a
+    # trifurcating root, e.g. DS1's, both give the same shape and numbering)
+    if len(tree.seed_node.child_nodes()) > 2:
+        tree.reroot_at_edge(tree.seed_node.child_nodes()[0].edge)
     dataio.setup_indexes(tree)
     dataio.setup_dates(tree, arg.dates, arg.heterochronous)
     stan_io.convert_samples_to_nexus(tree, arg.samples, arg.output, arg.rate)

@@ -18,6 +18,13 @@ restates the parts of its behaviour the data layout depends on:
   (dependency absent, version unpinned in ``setup.py:28``): the likelihood is
   invariant to it, only internal node numbering could differ -- documented as
   parity-unpinned in DESIGN.md.
+* ``reroot_at_edge(edge)`` (what ``phylostan parse`` does to a root with more
+  than two children, ``phylostan.py:140-141``): DendroPy 4's algorithm -- a
+  new node is appended to the edge's tail, the head moves under it, and the
+  tree is reseeded there, so the new root's children are [head, old root]
+  and the old root keeps its other children in order.  For a trifurcating
+  root (A, B, C) that is (A, (B, C)): the shape -- and node numbering --
+  ``resolve_polytomies`` gives ``run``.
 """
 import re
 
@@ -125,6 +132,30 @@ class Tree:
 
     def leaf_node_iter(self):
         return (n for n in self.seed_node.preorder_iter() if n.is_leaf())
+
+    def reroot_at_edge(self, edge, length1=None, length2=None, update_bipartitions=False):
+        """DendroPy's ``Tree.reroot_at_edge`` for an edge below the current
+        root (the only use: ``phylostan.py:141``).  The split edge's two
+        pieces get ``length1`` (new root -> old root) and ``length2`` (new
+        root -> head)."""
+        head = edge._node
+        tail = head.parent_node
+        if tail is None or tail is not self.seed_node:
+            raise ValueError("reroot_at_edge: only edges below the root are supported")
+        new_seed = Node(edge_length=length1)
+        tail.add_child(new_seed)
+        tail.remove_child(head)
+        new_seed.add_child(head)
+        head.edge_length = length2
+        # reseed: the old root becomes the last child of the new seed
+        tail.remove_child(new_seed)
+        tail.edge_length = new_seed.edge_length
+        new_seed.edge_length = None
+        new_seed.add_child(tail)
+        self.seed_node = new_seed
+
+    def adjacent_nodes(self):
+        return self.seed_node.child_nodes()
 
     def resolve_polytomies(self, limit=2, update_bipartitions=False):
         polytomies = [n for n in self.postorder_node_iter() if len(n._children) > limit]

@@ -236,3 +236,33 @@ def test_compiled_model_artifact(tmp_path):
         fp.write(b"\x80\x04\x95\x10\x00\x00\x00\x00\x00\x00\x00\xff\xfe")
     with pytest.raises(SystemExit):
         cli.load_artifact(str(tmp_path / "p.stan"))
+
+
+def test_parse_reroots_a_multifurcating_root_like_the_reference():
+    """phylostan.py:140-141: parse reroots a root with > 2 children at its
+    first child's edge (DendroPy reroot_at_edge: new root (head, old root),
+    the old root keeping its other children in order).  For a trifurcating
+    root that is the shape -- and the node numbering -- run's
+    resolve_polytomies gives (phylostan.py:175), so the sample columns of an
+    unrooted run map to the same nodes."""
+    from phylostan_amd import data as dataio
+    from phylostan_amd import treeio
+
+    def numbering(tree):
+        dataio.setup_indexes(tree)
+        return [(n.index, sorted(c.index for c in n.child_node_iter())) for n in tree.postorder_node_iter()
+                if not n.is_leaf()]
+
+    text = "((a:1,b:1):1,(c:1,d:1):1,e:2);"
+    t1 = treeio.parse_newick(text)
+    t1.resolve_polytomies()
+    t2 = treeio.parse_newick(text)
+    assert len(t2.seed_node.child_nodes()) == 3
+    t2.reroot_at_edge(t2.seed_node.child_nodes()[0].edge)
+    assert len(t2.seed_node.child_nodes()) == 2
+    assert numbering(t1) == numbering(t2)
+    # a four-way root keeps a trifurcation under the new root, as the reference does
+    t3 = treeio.parse_newick("(a:1,b:1,c:1,d:1);")
+    t3.reroot_at_edge(t3.seed_node.child_nodes()[0].edge)
+    kids = t3.seed_node.child_nodes()
+    assert kids[0].taxon.label == "a" and [c.taxon.label for c in kids[1].child_nodes()] == ["b", "c", "d"]
