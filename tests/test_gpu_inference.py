@@ -107,15 +107,19 @@ def test_fluA_nuts_short_multichain():
 def test_fluA_fullrank_advi_runs_to_convergence(tmp_path):
     """-q fullrank (phylostan.py:311-313 algorithm='fullrank') with the
     reference's defaults (adapted eta, tol_rel_obj 0.001, 100000 iterations)
-    on fluA: Stan's normal_fullrank SGA runs on GPU gradients until its
-    relative-ELBO test stops it, and writes the mean row plus 1000 draws.
+    on fluA: Stan's normal_fullrank SGA on GPU gradients runs until its
+    relative-ELBO test stops it, writes the mean row plus 1000 draws, and its
+    posterior means land inside the 95% intervals the reference prints for
+    meanfield (README.md:104-108; the README quotes meanfield only).
 
-    Measured: eta adaptation picks 0.1 and the median relative ELBO change
-    drops below 0.001 near iteration 35,000 at ELBO ~ -4,880, short of the
-    meanfield optimum (the clock rate is still ~0.14 against the README's
-    0.005), and a fixed eta = 1 diverges (every gradient draw non-finite).
-    The reference's README quotes meanfield only, so this test checks the
-    run and the ELBO trace, not the README intervals."""
+    Measured (round 3): eta adaptation picks 0.1, the median relative ELBO
+    change falls below 0.001 at iteration 4,100 (ELBO -11,390 at 100 ->
+    -4,430), 2 s.  The round-2 build of the same algorithm stalled near
+    iteration 35,000 at ELBO -4,880 (clock rate 0.14): the SGA path is
+    sensitive to the last bits of the gradient (the Q-parameter chain rule
+    was regrouped this round), the algorithm itself is pinned on CPU
+    (tests/test_inference.py: FullRank recovers a correlated Gaussian's
+    covariance; its gradient matches finite differences)."""
     from phylostan_amd import cli, stan_io
     t, a = fixture_files.write_dataset("fluA", str(tmp_path))
     out = str(tmp_path / "fluA_fr")
@@ -127,5 +131,9 @@ def test_fluA_fullrank_advi_runs_to_convergence(tmp_path):
     with open(out + ".diag") as fp:
         rows = [ln.strip().split(",") for ln in fp if ln.strip() and not ln.startswith(("#", "iter"))]
     elbo = np.array([float(r[2]) for r in rows])
-    assert np.isfinite(elbo).all() and elbo[-1] > elbo[0] + 10000.0
+    assert np.isfinite(elbo).all() and elbo[-1] > elbo[0] + 5000.0
     assert len(elbo) < 1000  # stopped by tol_rel_obj, not by the iteration cap
+    res = stan_io.parse_log(out, 0.05)
+    for key, (lo, hi) in README_CI.items():
+        m = res[key][0]
+        assert lo <= m <= hi, "%s mean %g outside the reference's 95%% CI (%g, %g)" % (key, m, lo, hi)
