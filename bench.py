@@ -35,6 +35,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 PEAK_HBM_GBPS = 8000.0  # MI355X_MICROARCH.md chip table: HBM3E 8.0 TB/s spec
+PEAK_FP64_TFLOPS = 78.6  # MI355X fp64 vector peak (no MFMA on this path)
 
 
 def parse():
@@ -508,6 +509,30 @@ def main():
         except (OSError, ValueError):
             traffic = None
 
+    # compute side of the same kernel (rocprofv3 SQ counters, tools/pmc_sq.py,
+    # same kernel source only): fp64 FLOP rate against the vector peak and
+    # the VALU's busy fraction -- the sweep is issue/latency-bound at two
+    # waves per SIMD, not HBM-bound
+    compute = None
+    sqp = os.path.join(ROOT, "profiles", "sq_counters.json")
+    if os.path.exists(sqp) and info["engine"] == "pattern" and batched:
+        try:
+            rec = json.load(open(sqp))
+            sq = rec.get("per_launch", {}).get("%s:pattern" % args.workload)
+            if rec.get("kernel_source") == kernel_source_hash() and sq:
+                flops = 64.0 * (2.0 * sq["SQ_INSTS_VALU_FMA_F64"] + sq["SQ_INSTS_VALU_MUL_F64"]
+                                + sq["SQ_INSTS_VALU_ADD_F64"])
+                t = kern_avg_ms * 1e-3
+                simd_cycles = t * 2.4e9 * 1024  # 256 CUs x 4 SIMDs at 2.4 GHz
+                compute = {"fp64_tflops": flops / t / 1e12, "fp64_peak_tflops": PEAK_FP64_TFLOPS,
+                           "fp64_frac": flops / t / 1e12 / PEAK_FP64_TFLOPS,
+                           "valu_busy": 4.0 * sq["SQ_ACTIVE_INST_VALU"] / simd_cycles,
+                           "instructions_per_wave": sq["SQ_INSTS"] / sq["SQ_WAVES"],
+                           "source": "profiles/sq_counters.json (rocprofv3 --pmc SQ counters of this kernel source; "
+                                     "SQ cycle counters in quad-cycles)"}
+        except (OSError, ValueError, KeyError):
+            compute = None
+
     cpu = cpu_mt = check = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:  # the CPU baseline is an N=1 figure
         hinfo = host_cpu_info()
@@ -550,6 +575,7 @@ def main():
                 "kernel": kernel_name, "kernel_avg_ms": kern_avg_ms,
                 "algorithmic_bytes_per_launch": alg,
                 "survey_model_bytes_per_launch": survey_bytes(S, P_local, C, draws),
+                "compute": compute,
             },
             "cpu_baseline": cpu,
             "cpu_baseline_all_threads": cpu_mt,

@@ -1267,6 +1267,7 @@ struct PmatArgs {
   double* pmat;           // [draw][C][nmat][R][4]  records, program-use order
   int C, B, kind, nmat, n, R;
   unsigned long long extra;  // tip masks of record vectors 4..R-1, 4 bits each
+  int with_eig;  // pmat_kernel forms the draw's eigensystem itself (small batches: no eig launch)
 };
 
 // Cyclic Jacobi eigendecomposition of a symmetric 4x4 (A overwritten).
@@ -1391,13 +1392,22 @@ __global__ void __launch_bounds__(64) eig_kernel(PmatArgs a) {
 // copies the 64 records out as one contiguous run (whole-line stores; a
 // record per lane straight to HBM would scatter every store instruction).
 constexpr int PMAT_WAVE_RECS = 64;
+constexpr int EIG_FUSE_MAX = 32;  // draws per launch up to which pmat_kernel forms the eigensystems
 __global__ void __launch_bounds__(64) pmat_kernel(PmatArgs a) {
   __shared__ double e[EIG_LEN];
   extern __shared__ __attribute__((aligned(16))) double recl[];  // [64][R*4]
   const int draw = blockIdx.y;
   const int C = a.C, nmat = a.nmat;
   const int lane = threadIdx.x;
-  if (lane < EIG_LEN) e[lane] = a.eig[(size_t)draw * EIG_LEN + lane];
+  if (a.with_eig) {  // a serial chain of one thread: every wave of the draw forms it (no eig launch)
+    if (lane == 0) {
+      eig_record(a.model + (size_t)draw * (10 + 2 * C), a.kind, e);
+      if (blockIdx.x == 0)
+        for (int k = 0; k < EIG_LEN; ++k) a.eig[(size_t)draw * EIG_LEN + k] = e[k];
+    }
+  } else if (lane < EIG_LEN) {
+    e[lane] = a.eig[(size_t)draw * EIG_LEN + lane];
+  }
   __syncthreads();
   const int total = C * nmat;
   const int idx0 = blockIdx.x * PMAT_WAVE_RECS;
@@ -1435,6 +1445,8 @@ struct FinArgs {
   double* grows;        // dL/dP rows (see SweepArgs)
   long long grows_stride;
   int kind;
+  int gsum_in;  // finalize_kernel first sums the gx per-workgroup dL/dP slots itself (few slots per draw)
+  int qf;       // finalize_kernel then runs the Q-parameter chain rule (qgrad_body)
 };
 
 // dL/dP of a draw spread over several workgroups: out[draw][og + (c*B+b)*16
@@ -1474,10 +1486,12 @@ __global__ void __launch_bounds__(256) gsum_kernel(FinArgs a) {
   }
 }
 
-// One workgroup per draw (dL/dP rows already in place: sweep or gsum); 1024
-// threads when a draw has many scalar slots (launch_finalize), so the slot
-// sums are a few rounds of loads in flight instead of a long latency chain
-// (the synthetic workload's 2,063 root chunks: 38 us with 256 threads).
+// One 1,024-thread workgroup per draw (dL/dP rows already in place: sweep or
+// gsum, or summed here first when a draw spans few workgroups -- gsum_in),
+// so the slot sums are a few rounds of loads in flight instead of a long
+// latency chain (the synthetic workload's 2,063 root chunks: 38 us with 256
+// threads); then, with qf, the Q-parameter chain rule: one launch for the
+// whole epilogue of a small batch.
 //   scalars log L, dlogL/dps, root-frequency term: wave 0, lane-strided
 //           over slots + a fixed-shape wave reduction;
 //   chain rule  dlogL/dt_{b,c} = <G_bc, Q P_bc>,  dlogL/db = sum_c r_c (.),
@@ -1490,6 +1504,21 @@ __global__ void __launch_bounds__(1024) finalize_kernel(FinArgs a) {
   double* Q = fsh + (size_t)C * B;
   double* out = a.out + (size_t)draw * a.outlen;
   const size_t wg0 = (size_t)draw * a.gx;
+  if (a.gsum_in) {
+    // the draw's dL/dP rows from its gx workgroup slots, summed in slot
+    // order (gsum_kernel's work, for draws spread over a few workgroups);
+    // made visible to the workgroup by the barriers below
+    const size_t per_wg = (size_t)C * a.nmat * 16;
+    const double* base = a.gslot + (size_t)draw * a.gx * per_wg;
+    for (int idx = threadIdx.x; idx < C * B * 16; idx += blockDim.x) {
+      const int c = idx / (B * 16), rem = idx - c * B * 16;
+      const int b = rem >> 4, k = rem & 15;
+      const double* src = base + ((size_t)c * a.nmat + a.gpos[b]) * 16 + k;
+      double s = src[0];
+      for (int w = 1; w < a.gx; ++w) s += src[(size_t)w * per_wg];
+      a.grows[(size_t)draw * a.grows_stride + idx] = s;
+    }
+  }
   if (threadIdx.x < 16) Q[threadIdx.x] = a.eig[(size_t)draw * EIG_LEN + EIG_Q + threadIdx.x];
   {
     // scalar partials per slot: [c][8] = ll (c = 0 only), dps_c, dfreq[4].
@@ -1578,6 +1607,11 @@ __global__ void __launch_bounds__(1024) finalize_kernel(FinArgs a) {
     double s = 0.0;
     for (int b = 0; b < B; ++b) s = fma(bl[b], inner[c * B + b], s);
     out[1 + B + c] = s;
+  }
+  if (a.qf) {  // the Q-parameter chain rule (qgrad_kernel's work, same bits)
+    __syncthreads();  // the finalize's root term visible to thread 0 of qgrad_body
+    const QgArgs q{a.eig, a.model, a.blens, a.grows, a.grows_stride, a.out, a.outlen, C, B, a.kind};
+    qgrad_body(q, draw, threadIdx.x, fsh + (size_t)C * B + 16 + blockDim.x);
   }
 }
 
@@ -2155,7 +2189,7 @@ int launch_class(phy_ctx* ctx, int n, const double* d_blens, const double* d_mod
                        (const double*)e->d_sitecls, (const int*)e->d_pat_root, d_site, ctx->P, e->nroot);
   FinArgs fa{ctx->d_gslot, e->d_sslot, ctx->d_pmat, ctx->d_eig, d_blens, d_model, ctx->d_gpos, ctx->d_inner, d_out,
              C,            B,          ctx->nmat,   e->nrootch,  phy_output_len(ctx), 0, ctx->R, grows, gstride,
-             ctx->kind};
+             ctx->kind,    0,          ctx->qfuse_pref ? 1 : 0};
   launch_finalize(fa, n, st);
   HIP_TRY(hipGetLastError());
   return PHY_OK;
@@ -2165,9 +2199,9 @@ int launch_pattern(phy_ctx* ctx, int n, const double* d_blens, const double* d_m
                    double* d_site, hipStream_t st, double* grows, long long gstride, bool* qdone = nullptr);
 
 void launch_finalize(const FinArgs& fa, int n, hipStream_t st) {
-  const int threads = fa.gx > 64 ? 1024 : 256;
-  hipLaunchKernelGGL(finalize_kernel, dim3(n), dim3(threads), ((size_t)fa.C * fa.B + 16 + threads) * sizeof(double),
-                     st, fa);
+  const int threads = 1024;
+  hipLaunchKernelGGL(finalize_kernel, dim3(n), dim3(threads),
+                     ((size_t)fa.C * fa.B + 16 + threads + (fa.qf ? QG_SHARED : 0)) * sizeof(double), st, fa);
 }
 
 // The resident class sweep (resident_engine.inc): forward + root L, then the
@@ -2193,7 +2227,7 @@ int launch_res(phy_ctx* ctx, int n, const double* d_blens, const double* d_model
                        (const double*)e->d_sitecls, (const int*)e->d_pat_root, d_site, ctx->P, e->nroot);
   FinArgs fa{ctx->d_gslot, e->d_sslot, ctx->d_pmat, ctx->d_eig, d_blens, d_model, ctx->d_gpos, ctx->d_inner, d_out,
              C,            B,          ctx->nmat,   1,           phy_output_len(ctx), 0, ctx->R, grows, gstride,
-             ctx->kind};
+             ctx->kind,    0,          ctx->qfuse_pref ? 1 : 0};
   launch_finalize(fa, n, st);
   HIP_TRY(hipGetLastError());
   return PHY_OK;
@@ -2203,17 +2237,24 @@ int launch(phy_ctx* ctx, int n, const double* d_blens, const double* d_model, do
            double* d_site, hipStream_t st) {
   const int C = ctx->C, B = ctx->B;
   {
+    // small batches: each pmat wave forms its draw's eigensystem (one launch
+    // less on the sampler's path); large ones: one thread per draw first
+    const int with_eig = n <= EIG_FUSE_MAX ? 1 : 0;
     PmatArgs pa{d_model, d_blens, ctx->d_mat_branch, ctx->d_eig, ctx->d_pmat, C, B, ctx->kind, ctx->nmat, n,
-                ctx->R, ctx->extra};
-    hipLaunchKernelGGL(eig_kernel, dim3((n + 63) / 64), dim3(64), 0, st, pa);
-    HIP_TRY(hipGetLastError());
+                ctx->R, ctx->extra, with_eig};
+    if (!with_eig) {
+      hipLaunchKernelGGL(eig_kernel, dim3((n + 63) / 64), dim3(64), 0, st, pa);
+      HIP_TRY(hipGetLastError());
+    }
     hipLaunchKernelGGL(pmat_kernel, dim3((C * ctx->nmat + PMAT_WAVE_RECS - 1) / PMAT_WAVE_RECS, n), dim3(64),
                        (size_t)PMAT_WAVE_RECS * ctx->R * 4 * sizeof(double), st, pa);
     HIP_TRY(hipGetLastError());
   }
   double* grows = ctx->compact ? ctx->d_grows : d_out + PHY_OUT_G(B, C);
   const long long gstride = ctx->compact ? (long long)16 * C * B : (long long)phy_output_len(ctx);
-  bool qdone = false;
+  // the chain rule runs inside the sweep (one workgroup per draw) or the
+  // finalize kernel unless PHY_QFUSE=0
+  bool qdone = ctx->qfuse_pref && ctx->engine != 0;
   int rc0 = ctx->engine == 1   ? launch_class(ctx, n, d_blens, d_model, d_out, d_site, st, grows, gstride)
             : ctx->engine == 2 ? launch_res(ctx, n, d_blens, d_model, d_out, d_site, st, grows, gstride)
                                : launch_pattern(ctx, n, d_blens, d_model, d_out, d_site, st, grows, gstride, &qdone);
@@ -2263,10 +2304,14 @@ int launch_pattern(phy_ctx* ctx, int n, const double* d_blens, const double* d_m
   }
   HIP_TRY(hipGetLastError());
   if (ctx->timing) HIP_TRY(hipEventRecord(e1, st));
+  // a draw over a few workgroups: the finalize sums their slots itself
+  // (one epilogue launch: slot sums, finalize, chain rule); over many, the
+  // wide gsum kernel first
+  const int gsum_in = (!g_direct && gx <= 16) ? 1 : 0;
   FinArgs fa{ctx->d_gslot, ctx->d_sslot, ctx->d_pmat, ctx->d_eig, d_blens, d_model, ctx->d_gpos, ctx->d_inner, d_out,
              C,            B,            ctx->nmat,   gx,          phy_output_len(ctx), g_direct, ctx->R, grows, gstride,
-             ctx->kind};
-  if (!g_direct) {
+             ctx->kind,    gsum_in,      (!fin && ctx->qfuse_pref) ? 1 : 0};
+  if (!g_direct && !gsum_in) {
     hipLaunchKernelGGL(gsum_kernel, dim3((C * B * 16 + 63) / 64, n), dim3(256), 0, st, fa);
     HIP_TRY(hipGetLastError());
   }
@@ -2274,7 +2319,7 @@ int launch_pattern(phy_ctx* ctx, int n, const double* d_blens, const double* d_m
     launch_finalize(fa, n, st);
     HIP_TRY(hipGetLastError());
   }
-  if (qdone) *qdone = qf != 0;
+  if (qdone) *qdone = qf != 0 || fa.qf != 0;
   return PHY_OK;
 }
 

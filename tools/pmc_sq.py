@@ -55,6 +55,24 @@ def main():
         for cn, v in acc.items():
             out[cn] = v / max(nev.get(cn, 1), 1)
     print(json.dumps(out, indent=1))
+    # keyed record for bench.py's roofline.compute (same kernel source only)
+    if not os.environ.get("PMC_KERNEL") and "SQ_INSTS_VALU_FMA_F64" in out and "SQ_WAVE_CYCLES" in out:
+        sys.path.insert(0, ROOT)
+        from bench import kernel_source_hash
+        wl = bench_args[bench_args.index("--workload") + 1] if "--workload" in bench_args else "fluA"
+        eng = bench_args[bench_args.index("--engine") + 1] if "--engine" in bench_args else "pattern"
+        path = os.path.join(ROOT, "profiles", "sq_counters.json")
+        rec = {}
+        if os.path.exists(path):
+            try:
+                rec = json.load(open(path))
+            except ValueError:
+                rec = {}
+        if rec.get("kernel_source") != kernel_source_hash():
+            rec = {"kernel_source": kernel_source_hash(), "per_launch": {}}
+        rec["per_launch"]["%s:%s" % (wl, eng)] = out
+        with open(path, "w") as fp:
+            json.dump(rec, fp, indent=1)
 
 
 if __name__ == "__main__":
