@@ -105,10 +105,14 @@ def _reversible_p_matrices(freqs, R, blens, rs):
     m2 = eigenvectors.T @ P2
     pmats = np.zeros((bcount * C, 4, 4))
     index = 0
-    for c in range(C):
-        for b in range(bcount):
-            pmats[index] = m1 @ np.diag(np.exp(eigenvalues * blens[b] * rs[c])) @ m2
-            index += 1
+    # an extreme draw (a branch of ~1e300) overflows e^(lambda t) for the
+    # round-off-positive zero eigenvalue: non-finite P, a rejected draw, as
+    # Stan's double arithmetic gives
+    with np.errstate(over="ignore", invalid="ignore"):
+        for c in range(C):
+            for b in range(bcount):
+                pmats[index] = m1 @ np.diag(np.exp(eigenvalues * blens[b] * rs[c])) @ m2
+                index += 1
     return pmats, Q
 
 

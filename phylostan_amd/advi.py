@@ -167,11 +167,14 @@ class ADVI:
         elementwise (stochastic_gradient_ascent: history 0.9 / 0.1, tau 1)."""
         es = eta / math.sqrt(it)
         for x, g, h in zip(q.params(), grads, hists):
-            if first:
-                h += g * g
-            else:
-                h *= 0.9
-                h += 0.1 * g * g
+            # a gradient beyond ~1e154 squares to inf here, as in Stan's
+            # Eigen arithmetic; that coordinate's step is then 0
+            with np.errstate(over="ignore"):
+                if first:
+                    h += g * g
+                else:
+                    h *= 0.9
+                    h += 0.1 * g * g
             x += es * g / (1.0 + np.sqrt(h))
 
     # ------------------------------------------------------------ phases

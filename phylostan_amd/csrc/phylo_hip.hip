@@ -1931,7 +1931,16 @@ int waves_per_simd(int K) { return K == 2 ? PHY_WPE2 : 4; }  // the kernel's reg
 // whole program).  An explicit budget (lds_budget) fixes the LDS share.
 // A chunk holds >= 3 matrices (one step uses up to three).
 int plan_chunks(phy_ctx* c) {
-  const int K = c->cols_pref ? c->cols_pref : (c->C <= 8 ? 2 : 1);
+  // automatic: two columns per lane, unless even the one-column plan's
+  // largest launch has at most one wave per SIMD (a sampler's few draws):
+  // then nothing shares a SIMD, and one column per lane halves each wave's
+  // step body (fluA, 4 draws: 182 -> 167 us per call; 100 draws: K = 2 stays
+  // ahead, 220 against 235 us)
+  int K = c->cols_pref;
+  if (!K) {
+    K = c->C <= 8 ? 2 : 1;
+    if (K == 2 && (long)c->max_draws * nblk_for(c->P, 1) * c->C <= 4L * c->cu_count) K = 1;
+  }
   if (K == 2 && c->C > 8) return fail(PHY_EINVAL, "two columns per lane need C <= 8");
   if ((size_t)std::max(c->nslots, c->ndeep) * K * 2 * c->C * WAVE * 16 >= (size_t)OOB)
     return fail(PHY_EINVAL, "per-workgroup scratch region too large for 32-bit buffer offsets");

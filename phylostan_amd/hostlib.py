@@ -36,6 +36,16 @@ def load():
         for f in ("phh_heights", "phh_heights_back", "phh_height_jacobian", "phh_span", "phh_span_back",
                   "phh_constant_coalescent"):
             getattr(lib, f).restype = None
+        if hasattr(lib, "phh_strict_create"):
+            lib.phh_strict_create.argtypes = [_i, _i, _i, _i, _i, _i, ctypes.c_double, _i, _i, ctypes.c_double, _i,
+                                              _I, _i, _I, _I, _I, _D, _i, _I, _I, _D, _i, _I, _D, _D]
+            lib.phh_strict_create.restype = ctypes.c_void_p
+            lib.phh_strict_free.argtypes = [ctypes.c_void_p]
+            lib.phh_strict_free.restype = None
+            lib.phh_strict_pre.argtypes = [ctypes.c_void_p, _i, _D, _D, _D, _I]
+            lib.phh_strict_pre.restype = ctypes.c_int
+            lib.phh_strict_post.argtypes = [ctypes.c_void_p, _i, _D, _D, _i, _I, _i, _D, _D]
+            lib.phh_strict_post.restype = None
         _lib = lib
     return _lib
 
@@ -104,6 +114,58 @@ class ClockTreeNative:
     def span_back(self, gspan, gh):
         gspan = _c(gspan)
         self.lib.phh_span_back(gspan.shape[0], self.H, self.B, self.p_bpar, self.p_bh, _d(gspan), _d(gh))
+
+
+class StrictPosterior:
+    """The strict-clock log density + gradient around the likelihood in two
+    native phases (csrc/host_model.cpp phh_strict_*): ``pre`` maps draws U to
+    the branch lengths / model vectors of those that reach the likelihood,
+    ``post`` maps the likelihood's rows to (lp, G).  ``posterior.Posterior``
+    builds one for the specs it covers; its numpy path is the specification
+    (tests/test_hostlib.py compares the two)."""
+
+    def __init__(self, nat, S, B, C, model, weibull, est_rate, fixed_rate, coal, heterochronous, lower_root, dim,
+                 offsets, lowers):
+        self.lib = load()
+        self.nat = nat  # keeps the index arrays alive
+        self.B, self.C, self.dim = B, C, dim
+        self.ml = 10 + 2 * C
+        offs = _c(offsets, np.int32)
+        self.lowers = _c(lowers)
+        self.h = self.lib.phh_strict_create(
+            S, B, C, model, int(weibull), int(est_rate), float(fixed_rate), int(coal), int(heterochronous),
+            float(lower_root), dim, offs.ctypes.data, nat.m, nat.p_node, nat.p_par, nat.p_prop, nat.p_low, nat.root,
+            nat.p_bpar, nat.p_bh, nat.p_blow, len(nat.jpar), nat.p_jpar, nat.p_jlow, self.lowers.ctypes.data)
+        self._n = 0
+
+    def _buffers(self, n):
+        if n > self._n:
+            self._n = n
+            self.blens = np.empty((n, self.B))
+            self.mv = np.empty((n, self.ml))
+            self.sel = np.empty(n, np.int32)
+        return self.blens, self.mv, self.sel
+
+    def pre(self, U):
+        """U [n, dim] -> (count, blens [count, B], model vectors [count, ml], sel [n])."""
+        n = U.shape[0]
+        bl, mv, sel = self._buffers(n)
+        cnt = self.lib.phh_strict_pre(self.h, n, U.ctypes.data, bl.ctypes.data, mv.ctypes.data, sel.ctypes.data)
+        return cnt, bl[:cnt], mv[:cnt], sel[:n].copy()
+
+    def post(self, U, rows, sel, need_grad=True):
+        n = U.shape[0]
+        lp = np.empty(n)
+        G = np.empty((n, self.dim)) if need_grad else None
+        rows = _c(rows) if rows is not None and len(rows) else np.zeros((1, 1))
+        self.lib.phh_strict_post(self.h, n, U.ctypes.data, rows.ctypes.data, rows.shape[1], _c(sel, np.int32).ctypes.data,
+                                 int(need_grad), lp.ctypes.data, G.ctypes.data if need_grad else None)
+        return lp, G
+
+    def __del__(self):
+        if getattr(self, "h", None) and self.lib is not None:
+            self.lib.phh_strict_free(self.h)
+            self.h = None
 
 
 def constant_coalescent(times, internal, theta):

@@ -162,6 +162,29 @@ class Posterior:
         self.const = self._dropped_constants()
         i = np.arange(1, self.C + 1, dtype=np.float64)
         self._wx = -np.log(1.0 - (2.0 * (i - 1) + 1.0) / (2.0 * self.C))  # Weibull quantile bases
+        self._fast = self._native_strict()
+
+    def _native_strict(self):
+        """The native two-phase log density (hostlib.StrictPosterior) for the
+        strict-clock family it covers -- phylostan's default build (Weibull
+        or no site rates, any substitution model, estimated or fixed rate,
+        constant coalescent or none) -- else None (the numpy path below,
+        which stays the specification).  PHYLO_HOST_FAST=0 turns it off."""
+        sp = self.spec
+        lib = hostlib.load()
+        if (getattr(self, "_nat", None) is None or lib is None or not hasattr(lib, "phh_strict_create")
+                or os.environ.get("PHYLO_HOST_FAST", "1") == "0"):
+            return None
+        if (sp.clock != "strict" or sp.coalescent not in (None, "constant") or sp.speciation not in (None, "yule")
+                or sp.invariant or (sp.categories > 1 and sp.heterogeneity != "weibull") or self.C > 64):
+            return None
+        off = {p.name: p.sl.start for p in self.params}
+        names = ["wshape", "props", "rate", "height", "theta", "kappa", "rates", "freqs"]
+        offsets = [off.get(k, -1) for k in names]
+        fixed = sp.rate if sp.rate is not None else 1.0
+        return hostlib.StrictPosterior(self._nat, self.S, self.B, self.C, models.MODEL_IDS[sp.model],
+                                       sp.categories > 1, sp.estimate_rate, fixed, sp.coalescent == "constant",
+                                       sp.heterochronous, self.lower_root, self.dim, offsets, self.lowers)
 
     # ------------------------------------------------------------------ layout
     def _declare(self):
@@ -493,6 +516,17 @@ class Posterior:
         whose evaluation is started (asynchronously when the engine offers
         ``submit_rows``); ``log_prob_grad_end`` finishes.  Lets a sampler
         overlap one group of chains' host work with another's GPU work."""
+        if self._fast is not None:
+            U = np.ascontiguousarray(np.atleast_2d(U), np.float64)
+            cnt, bl, mv, sel = self._fast.pre(U)
+            tok = {"fast": True, "U": U, "sel": sel, "propto": propto, "need_grad": need_grad}
+            if cnt:
+                if hasattr(self.lik, "submit_rows") and cnt <= 64:
+                    self.lik.submit_rows(bl, mv)
+                    tok["async"] = True
+                else:
+                    tok["rows"] = self._lik_rows(bl, mv)
+            return tok
         U = np.atleast_2d(np.asarray(U, np.float64))
         n = U.shape[0]
         with np.errstate(all="ignore"):
@@ -517,6 +551,12 @@ class Posterior:
         return tok
 
     def log_prob_grad_end(self, tok):
+        if tok.get("fast"):
+            rows = self.lik.wait_rows() if tok.get("async") else tok.get("rows")
+            lp, G = self._fast.post(tok["U"], rows, tok["sel"], tok["need_grad"])
+            if not tok["propto"]:
+                lp = np.where(np.isfinite(lp), lp + self.const, lp)
+            return lp, G
         n, ok, need_grad = tok["n"], tok["ok"], tok["need_grad"]
         lp = np.full(n, -np.inf)
         G = np.zeros((n, self.dim)) if need_grad else None

@@ -22,7 +22,11 @@ def _log1p_exp(x):
 
 
 def _inv_logit(u):
-    return 0.5 * (1.0 + np.tanh(0.5 * u))  # overflow-free
+    """Stan Math's inv_logit: 1 / (1 + e^-u) for u >= 0, e^u / (1 + e^u)
+    below (overflow-free; 0 and 1 only where e^-|u| underflows against 1, so
+    the native host path, csrc/host_model.cpp, decides support alike)."""
+    e = np.exp(-np.abs(u))
+    return np.where(u >= 0, 1.0, e) / (1.0 + e)
 
 
 class Transform:

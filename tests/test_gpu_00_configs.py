@@ -111,9 +111,14 @@ def test_config_vs_reference_pruner(k):
     order = ["DS1", "fluA", "HCV"]
     pt = [p for p in pts if p["dataset"] == order[k]][0]
     case = cases.mixture_case(pt)
-    for engine in ("pattern", "class"):
+    # the pattern sweep under both plans: one column per lane (what a
+    # sampler's small context plans) and two (the batched bench's plan)
+    for engine, cols in (("pattern", 1), ("pattern", 2), ("class", 0)):
         eng = _engine(case)
         eng.set_engine(engine)
+        if cols:
+            eng.set_tuning(cols=cols)
+            assert eng.lds_plan()["cols"] == cols
         res = eng.evaluate(case.blens, case.model_vec(), site_ll=True)
         ref = case.oracle()
         e = errors(res, ref, case.model)
@@ -123,7 +128,8 @@ def test_config_vs_reference_pruner(k):
         e_ref_ll = abs(res.loglik - pt["loglik"]) / abs(pt["loglik"])
         assert e_ref_site <= RTOL_LL and e_ref_ll <= RTOL_LL, (e_ref_site, e_ref_ll)
         report.record("%s [%s]: vs scripts/phylo.py loglik %.1e site_ll %.1e | vs oracle %s  Q-params %.1e"
-                      % (MIXTURE_IDS[pt["dataset"]], engine, e_ref_ll, e_ref_site, fmt(e), eq))
+                      % (MIXTURE_IDS[pt["dataset"]], engine + (" K=%d" % cols if cols else ""), e_ref_ll,
+                         e_ref_site, fmt(e), eq))
 
 
 @pytest.mark.parametrize("k", range(4))

@@ -49,8 +49,10 @@ def _posterior(name, **kw):
 def test_native_posterior_equals_numpy(name, kw):
     post = _posterior(name, **kw)
     assert post._nat is not None
+    post._fast = None  # the native loops inside the numpy path
     ref = _posterior(name, **kw)
     ref._nat = None
+    ref._fast = None
     rng = np.random.default_rng(3)
     U = np.stack([post.initial_point(rng) for _ in range(5)])
     lp_n, g_n = post.log_prob_grad(U)
@@ -75,3 +77,85 @@ def test_native_constant_coalescent_equals_numpy():
     b = priors.constant_coalescent(times, internal, theta)
     for x, y in zip(a, b):
         np.testing.assert_allclose(x, y, rtol=1e-12, atol=1e-12)
+
+
+class RowsLik:
+    """Deterministic compact output rows from (blens, model vectors), every
+    entry non-zero -- the Q-parameter and site-rate gradients included."""
+
+    def __init__(self, B, C):
+        self.B, self.C = B, C
+        self.calls = 0
+
+    def evaluate_rows(self, blens, mv):
+        self.calls += 1
+        B, C = self.B, self.C
+        o = 1 + B + 2 * C
+        rows = np.empty((blens.shape[0], o + 14))
+        lb = np.log(blens)
+        rows[:, 0] = -0.5 * np.sum((lb + 3.0) ** 2, axis=1) + np.log(mv[:, 10:10 + C]).sum(axis=1)
+        rows[:, 1:1 + B] = -(lb + 3.0) / blens
+        rows[:, 1 + B:o] = np.cos(mv[:, 10:10 + 2 * C]) + 0.5
+        rows[:, o:o + 4] = np.sin(mv[:, :4]) * 3.0
+        rows[:, o + 4:o + 10] = np.cos(3.0 * mv[:, 4:10])
+        rows[:, o + 10:o + 14] = np.sin(2.0 * mv[:, :4]) - 0.25
+        return rows
+
+
+FAST_SPECS = [
+    ("fluA", dict(model="HKY", categories=4, clock="strict", estimate_rate=True, coalescent="constant",
+                  heterochronous=True)),  # config 5, phylostan's default build
+    ("fluA", dict(model="GTR", categories=1, clock="strict", estimate_rate=False, rate=0.004, heterochronous=True)),
+    ("HCV", dict(model="JC69", categories=3, clock="strict", estimate_rate=True, coalescent="constant")),
+    ("HCV", dict(model="GTR", categories=4, clock="strict", estimate_rate=False, coalescent="constant",
+                 speciation="yule")),
+]
+
+
+@pytest.mark.parametrize("name,kw", FAST_SPECS, ids=["fluA_HKY4_rate_const_het", "fluA_GTR1_fixed",
+                                                     "HCV_JC3_rate_const", "HCV_GTR4_fixed_const_yule"])
+def test_native_strict_posterior_equals_numpy(name, kw):
+    """hostlib.StrictPosterior (both phases native) against the numpy
+    specification: log density (propto and not) and gradient, including
+    out-of-support and non-finite draws (lp = -inf, zero gradient)."""
+    def make():
+        d = cases.load_layout(name)
+        S = d["tipbits"].shape[0]
+        tree = TreeData(S, d["peel"] - 1, d["map"], d.get("lowers"), float(d["oldest"]) if "oldest" in d else None)
+        spec = ModelSpec(**kw)
+        return Posterior(spec, tree, RowsLik(2 * S - 2, spec.C))
+    post, ref = make(), make()
+    assert post._fast is not None
+    ref._fast = None
+    rng = np.random.default_rng(11)
+    U = np.stack([post.initial_point(rng) for _ in range(7)])
+    U[2, post.param("props").sl.start + 3] = 40.0   # props -> 1.0 exactly: out of support
+    U[4, post.param("height").sl.start] = np.nan    # non-finite
+    U[5] *= 0.1
+    for propto in (True, False):
+        lp_n, g_n = post.log_prob_grad(U, propto=propto)
+        lp_r, g_r = ref.log_prob_grad(U, propto=propto)
+        assert np.array_equal(np.isfinite(lp_n), np.isfinite(lp_r))
+        assert not np.isfinite(lp_n[2]) and not np.isfinite(lp_n[4])
+        fin = np.isfinite(lp_r)
+        np.testing.assert_allclose(lp_n[fin], lp_r[fin], rtol=1e-12)
+        np.testing.assert_allclose(g_n, g_r, rtol=1e-10, atol=1e-10 * np.abs(g_r).max())
+        assert not np.any(g_n[~fin])
+    lp_n, g_n = post.log_prob_grad(U, need_grad=False)
+    assert g_n is None and np.array_equal(np.isfinite(lp_n), np.isfinite(lp_r))
+    # the asynchronous pair (submit / wait) takes the same path
+    tok = post.log_prob_grad_begin(U)
+    lp_a, g_a = post.log_prob_grad_end(tok)
+    np.testing.assert_array_equal(lp_a, post.log_prob_grad(U)[0])
+
+
+def test_native_strict_posterior_not_used_outside_its_family():
+    d = cases.load_layout("fluA")
+    S = d["tipbits"].shape[0]
+    tree = TreeData(S, d["peel"] - 1, d["map"], d.get("lowers"), float(d["oldest"]))
+    for kw in (dict(model="HKY", categories=4, invariant=True, clock="strict", estimate_rate=True),
+               dict(model="HKY", categories=4, clock="ucln", estimate_rate=True),
+               dict(model="HKY", categories=4, clock="strict", estimate_rate=True, coalescent="skyride"),
+               dict(model="HKY", categories=4)):
+        spec = ModelSpec(**kw)
+        assert Posterior(spec, tree, RowsLik(2 * S - 2, spec.C))._fast is None

@@ -20,6 +20,8 @@ def main():
     ap.add_argument("--calls", type=int, default=300)
     ap.add_argument("--workload", default="fluA", choices=["fluA", "HCV", "DS1"])
     ap.add_argument("--engine", default="auto", choices=["auto", "pattern", "class", "resident"])
+    ap.add_argument("--cols", type=int, default=0, help="pattern columns per lane (0 = the plan's choice)")
+    ap.add_argument("--lds-budget", type=int, default=0)
     a = ap.parse_args()
     from phylostan_amd.engine import TreeLikelihood
     from tests import cases
@@ -29,15 +31,18 @@ def main():
     lik.set_output(compact=True)
     if a.engine != "auto":
         lik.set_engine(a.engine)
+    if a.cols or a.lds_budget:
+        lik.set_tuning(cols=a.cols, lds_budget=a.lds_budget)
     bl = np.stack([case.blens * (1.0 + 0.01 * k) for k in range(a.draws)])
     mv = np.stack([case.model_vec()] * a.draws)
     for _ in range(20):
-        lik.evaluate_batch(bl, mv)
+        lik.evaluate_rows(bl, mv)
     t0 = time.perf_counter()
     for _ in range(a.calls):
-        lik.evaluate_batch(bl, mv)
+        lik.evaluate_rows(bl, mv)
     dt = (time.perf_counter() - t0) / a.calls
-    print(json.dumps({"workload": a.workload, "engine": lik.engine(), "draws": a.draws, "us_per_call": dt * 1e6}))
+    print(json.dumps({"workload": a.workload, "engine": lik.engine(), "draws": a.draws, "cols": a.cols,
+                      "lds_budget": a.lds_budget, "us_per_call": dt * 1e6}))
 
 
 if __name__ == "__main__":
