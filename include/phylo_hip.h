@@ -201,6 +201,18 @@ int phy_deep_stack_in_lds(const phy_ctx* ctx);
  * phy_recomputed_partials: moved partials per column the current plan does
  * not store. */
 int phy_set_recompute(phy_ctx* ctx, int on);
+
+/* HIP graphs (default off; PHY_GRAPH=1 at phy_create turns them on): an
+ * evaluation whose operands (draw count, buffers, stream) repeat is
+ * captured once -- its copies and every kernel launch, up to ~50 for the
+ * class sweep -- and replayed as one graph launch.  The first run of an
+ * operand set is direct, the second captures; any replan, output-layout or
+ * engine change rebuilds.  Evaluations under phy_timing_start run direct.
+ * Results are identical either way.  Measured on MI355X: no gain (a 4-draw
+ * call 167 -> 174 us; the class sweep's ~50 launches are bound by GPU-side
+ * gaps between dependent kernels, which a graph keeps).  No reference
+ * counterpart (a launch mechanism). */
+int phy_set_graphs(phy_ctx* ctx, int on);
 int phy_recomputed_partials(const phy_ctx* ctx);
 
 /* Output rows: compact = 1 drops the dL/dP block (rows end after the

@@ -49,6 +49,7 @@ SIGNATURES = {
     "phy_set_deep_stack": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
     "phy_deep_stack_in_lds": (ctypes.c_int, [ctypes.c_void_p]),
     "phy_set_recompute": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
+    "phy_set_graphs": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
     "phy_recomputed_partials": (ctypes.c_int, [ctypes.c_void_p]),
     "phy_set_engine": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
     "phy_set_output": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),

@@ -1691,6 +1691,19 @@ struct phy_ctx {
   double* d_gslot = nullptr;
   double* d_sslot = nullptr;
   bool timing = false;
+  // HIP graphs of whole evaluations (launch_graphed): one per operand set,
+  // replayed while plan_gen (bumped by every plan / buffer / engine change)
+  // is unchanged; PHY_GRAPH=0 turns them off
+  struct Graph {
+    int n;
+    const void *bl, *md, *out, *site, *st;
+    long gen;
+    hipGraphExec_t ex;
+  };
+  std::vector<Graph> graphs;
+  Graph seen{};                // the last operand set run directly: captured when it comes again
+  long plan_gen = 0;
+  bool graph_pref = false;     // measured no gain: opt-in
   std::vector<hipEvent_t> ev;  // pairs
   int ev_used = 0;
   double timed_ms = 0.0;
@@ -1712,6 +1725,7 @@ void free_ctx(phy_ctx* c) {
   if (c->h_in) (void)hipHostFree(c->h_in);
   if (c->h_out) (void)hipHostFree(c->h_out);
   for (hipEvent_t e : c->ev) (void)hipEventDestroy(e);
+  for (auto& g : c->graphs) (void)hipGraphExecDestroy(g.ex);
   free_class_engine(c->ce);
   free_res_engine(c->re);
   free_multi(c->ms);
@@ -1987,6 +2001,7 @@ int plan_chunks(phy_ctx* c) {
   if (lds > LDS_CAP) return fail(PHY_EINVAL, "tree too large for LDS (tips of one block)");
   c->K = K;
   c->nblk = nb;
+  ++c->plan_gen;
   c->wg_resident = c->cu_count * std::min<int>(by_waves, (int)(LDS_CAP / lds));
   {
     // workgroup regions the largest launch of this plan may use
@@ -2085,6 +2100,7 @@ int ensure_res_plan(phy_ctx* c) {
 }
 
 int select_engine(phy_ctx* c) {
+  ++c->plan_gen;
   c->engine = 0;
   if (c->engine_pref == 1) return PHY_OK;
   if (c->engine_pref == 3) {
@@ -2278,6 +2294,79 @@ int launch(phy_ctx* ctx, int n, const double* d_blens, const double* d_model, do
   return PHY_OK;
 }
 
+// One evaluation's stream work (`body`: launch(), with the small path's
+// copies around it) through a HIP graph (opt-in: phy_set_graphs; measured
+// on MI355X, a 4-draw fluA call 167 -> 174 us, the synthetic shard-8
+// projection 3251 -> 3273 evals/s -- the class sweep is bound by the
+// GPU-side gaps between its dependent kernels, which a graph keeps, not by
+// host launch cost): the first run of an operand set
+// (draw count, buffers, stream) is direct -- it makes any lazy allocation
+// (class / resident reserves) -- the second is captured and instantiated,
+// later ones replay it: one graph launch instead of up to ~50 kernel
+// launches (the class sweep's levels).  Engine reserves are grown before
+// the lookup; growth or any replan bumps plan_gen, and stale graphs are
+// rebuilt.  Timed evaluations (phy_timing_*) and a failed capture run
+// direct.
+template <typename F>
+int launch_graphed(phy_ctx* ctx, int n, const void* bl, const void* md, const void* out, const void* site,
+                   hipStream_t st, F&& body) {
+  if (!ctx->graph_pref || ctx->timing) return body();
+  {
+    int rc = PHY_OK;
+    if (ctx->engine == 1 && n > ctx->ce->max_draws) {
+      if ((rc = class_engine_reserve(ctx->ce, n))) return rc;
+      ++ctx->plan_gen;
+    } else if (ctx->engine == 2 && n > ctx->re->max_draws) {
+      if ((rc = res_engine_reserve(ctx->re, n))) return rc;
+      ++ctx->plan_gen;
+    }
+  }
+  const phy_ctx::Graph key{n, bl, md, out, site, (const void*)st, ctx->plan_gen, nullptr};
+  auto same = [&](const phy_ctx::Graph& g) {
+    return g.n == key.n && g.bl == key.bl && g.md == key.md && g.out == key.out && g.site == key.site &&
+           g.st == key.st && g.gen == key.gen;
+  };
+  for (auto& g : ctx->graphs)
+    if (same(g)) {
+      HIP_TRY(hipGraphLaunch(g.ex, st));
+      return PHY_OK;
+    }
+  if (!same(ctx->seen)) {  // first sighting: direct
+    ctx->seen = key;
+    return body();
+  }
+  // stale entries (older plans) go first, then the oldest beyond 8
+  for (size_t i = 0; i < ctx->graphs.size();)
+    if (ctx->graphs[i].gen != ctx->plan_gen) {
+      (void)hipGraphExecDestroy(ctx->graphs[i].ex);
+      ctx->graphs.erase(ctx->graphs.begin() + i);
+    } else {
+      ++i;
+    }
+  if (ctx->graphs.size() >= 8) {
+    (void)hipGraphExecDestroy(ctx->graphs.front().ex);
+    ctx->graphs.erase(ctx->graphs.begin());
+  }
+  HIP_TRY(hipStreamBeginCapture(st, hipStreamCaptureModeThreadLocal));
+  const int rc = body();
+  hipGraph_t g = nullptr;
+  const hipError_t ec = hipStreamEndCapture(st, &g);
+  hipGraphExec_t ex = nullptr;
+  hipError_t ei = hipErrorUnknown;
+  if (rc == PHY_OK && ec == hipSuccess && g) ei = hipGraphInstantiate(&ex, g, nullptr, nullptr, 0);
+  if (g) (void)hipGraphDestroy(g);
+  if (rc != PHY_OK || ec != hipSuccess || ei != hipSuccess) {  // run it direct, and stop capturing
+    (void)hipGetLastError();
+    ctx->graph_pref = false;
+    return body();
+  }
+  phy_ctx::Graph ent = key;
+  ent.ex = ex;
+  ctx->graphs.push_back(ent);
+  HIP_TRY(hipGraphLaunch(ex, st));
+  return PHY_OK;
+}
+
 // The pattern sweep (sweep_kernel) and its dL/dP sums / finalize.
 int launch_pattern(phy_ctx* ctx, int n, const double* d_blens, const double* d_model, double* d_out,
                    double* d_site, hipStream_t st, double* grows, long long gstride, bool* qdone) {
@@ -2444,6 +2533,8 @@ int phy_create(int S, int P, int C, int rooted, int model, const uint8_t* tipcod
     c->fin_pref = fk ? atoi(fk) != 0 : true;
     const char* qk = getenv("PHY_QFUSE");
     c->qfuse_pref = qk ? atoi(qk) != 0 : true;
+    const char* gk = getenv("PHY_GRAPH");
+    c->graph_pref = gk ? atoi(gk) != 0 : false;
 
   }
   hipError_t he = hipSetDevice(device);
@@ -2668,6 +2759,7 @@ int phy_set_output(phy_ctx* ctx, int compact) {
     if (rc) return rc;
   }
   ctx->compact = compact ? 1 : 0;
+  ++ctx->plan_gen;
   return PHY_OK;
 }
 
@@ -2691,7 +2783,8 @@ int phy_eval_device(phy_ctx* ctx, int n_draws, const double* d_blens, const doub
     return fail(PHY_EINVAL, "phy_eval_device: a phy_eval_submit is still in flight (phy_eval_wait first)");
   HIP_TRY(hipSetDevice(ctx->device));
   hipStream_t st = stream ? reinterpret_cast<hipStream_t>(stream) : ctx->stream;
-  return launch(ctx, n_draws, d_blens, d_model, d_out, d_site_ll, st);
+  return launch_graphed(ctx, n_draws, d_blens, d_model, d_out, d_site_ll, st,
+                        [&]() -> int { return launch(ctx, n_draws, d_blens, d_model, d_out, d_site_ll, st); });
 }
 
 // phy_eval_submit / phy_eval_wait: the small-batch path split at the stream
@@ -2719,10 +2812,14 @@ int phy_eval_submit(phy_ctx* ctx, int n_draws, const double* blens, const double
   const size_t no = (size_t)n_draws * phy_output_len(ctx);
   std::memcpy(ctx->h_in, blens, sizeof(double) * nb);
   std::memcpy(ctx->h_in + nb, model, sizeof(double) * nm);
-  HIP_TRY(hipMemcpyAsync(ctx->d_in, ctx->h_in, sizeof(double) * (nb + nm), hipMemcpyHostToDevice, st));
-  int rc = launch(ctx, n_draws, ctx->d_in, ctx->d_in + nb, ctx->d_out, nullptr, st);
+  int rc = launch_graphed(ctx, n_draws, ctx->h_in, ctx->d_in, ctx->h_out, nullptr, st, [&]() -> int {
+    HIP_TRY(hipMemcpyAsync(ctx->d_in, ctx->h_in, sizeof(double) * (nb + nm), hipMemcpyHostToDevice, st));
+    int r = launch(ctx, n_draws, ctx->d_in, ctx->d_in + nb, ctx->d_out, nullptr, st);
+    if (r) return r;
+    HIP_TRY(hipMemcpyAsync(ctx->h_out, ctx->d_out, sizeof(double) * no, hipMemcpyDeviceToHost, st));
+    return PHY_OK;
+  });
   if (rc) return rc;
-  HIP_TRY(hipMemcpyAsync(ctx->h_out, ctx->d_out, sizeof(double) * no, hipMemcpyDeviceToHost, st));
   ctx->pending = n_draws;
   return PHY_OK;
 }
@@ -2761,10 +2858,15 @@ int phy_eval(phy_ctx* ctx, int n_draws, const double* blens, const double* model
     const size_t no = (size_t)n_draws * phy_output_len(ctx);
     std::memcpy(ctx->h_in, blens, sizeof(double) * nb);
     std::memcpy(ctx->h_in + nb, model, sizeof(double) * nm);
-    HIP_TRY(hipMemcpyAsync(ctx->d_in, ctx->h_in, sizeof(double) * (nb + nm), hipMemcpyHostToDevice, st));
-    int rc = launch(ctx, n_draws, ctx->d_in, ctx->d_in + nb, ctx->d_out, site_ll ? ctx->d_site : nullptr, st);
+    double* dsite = site_ll ? ctx->d_site : nullptr;
+    int rc = launch_graphed(ctx, n_draws, ctx->h_in, ctx->d_in, ctx->h_out, dsite, st, [&]() -> int {
+      HIP_TRY(hipMemcpyAsync(ctx->d_in, ctx->h_in, sizeof(double) * (nb + nm), hipMemcpyHostToDevice, st));
+      int r = launch(ctx, n_draws, ctx->d_in, ctx->d_in + nb, ctx->d_out, dsite, st);
+      if (r) return r;
+      HIP_TRY(hipMemcpyAsync(ctx->h_out, ctx->d_out, sizeof(double) * no, hipMemcpyDeviceToHost, st));
+      return PHY_OK;
+    });
     if (rc) return rc;
-    HIP_TRY(hipMemcpyAsync(ctx->h_out, ctx->d_out, sizeof(double) * no, hipMemcpyDeviceToHost, st));
     if (site_ll)
       HIP_TRY(hipMemcpyAsync(site_ll, ctx->d_site, sizeof(double) * n_draws * ctx->P, hipMemcpyDeviceToHost, st));
     HIP_TRY(hipStreamSynchronize(st));
@@ -2901,6 +3003,19 @@ int phy_set_recompute(phy_ctx* ctx, int on) {
   return plan_chunks(ctx);
 }
 int phy_recomputed_partials(const phy_ctx* ctx) { return ctx ? (ctx->ms ? ctx->ms->shard[0]->nrec : ctx->nrec) : -1; }
+
+int phy_set_graphs(phy_ctx* ctx, int on) {
+  if (!ctx) return fail(PHY_EINVAL, "NULL ctx");
+  if (ctx->ms) {  // the shards launch direct; the flag is kept for phy_eval_* on this context
+    ctx->graph_pref = on != 0;
+    return PHY_OK;
+  }
+  HIP_TRY(hipSetDevice(ctx->device));
+  HIP_TRY(hipStreamSynchronize(ctx->stream));
+  ctx->graph_pref = on != 0;
+  ++ctx->plan_gen;
+  return PHY_OK;
+}
 
 int phy_set_engine(phy_ctx* ctx, int mode) {
   if (!ctx) return fail(PHY_EINVAL, "NULL ctx");

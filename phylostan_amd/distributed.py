@@ -55,6 +55,7 @@ class ShardedLikelihood:
         if self.p1 <= self.p0:
             raise ValueError("more ranks than patterns")
         if engine_factory is None:
+            import torch  # noqa: F401 -- torch's HIP runtime loads before the engine's
             from .engine import TreeLikelihood
             engine_factory = TreeLikelihood
         self.engine = engine_factory(np.ascontiguousarray(np.asarray(tipcodes)[:, self.p0:self.p1]),

@@ -212,6 +212,10 @@ class TreeLikelihood:
         """Deep-stack placement: 0 automatic, 1 LDS, 2 global (replans)."""
         _lib.check(self.lib.phy_set_deep_stack(self.ctx, int(mode)), "phy_set_deep_stack")
 
+    def set_graphs(self, on=True):
+        """Replay repeated evaluations from HIP graphs (phy_set_graphs)."""
+        _lib.check(self.lib.phy_set_graphs(self.ctx, int(bool(on))), "phy_set_graphs")
+
     def set_recompute(self, on=True):
         """Rebuild cherries in the reverse half instead of storing them (replans)."""
         _lib.check(self.lib.phy_set_recompute(self.ctx, int(bool(on))), "phy_set_recompute")
