@@ -25,6 +25,23 @@
 #include <omp.h>
 #endif
 
+/* Jacobi rotations in the parallel ordering -- per sweep three rounds of two
+ * rotations on disjoint index pairs {(0,1),(2,3)}, {(0,2),(1,3)}, {(0,3),(1,2)}:
+ * both rotations' parameters from the round's A, then A <- J^T A J (columns,
+ * then rows) and V <- V J.  The device (csrc/phylo_hip.hip jacobi4) runs the
+ * same operations in the same order, uncontracted: the same bits. */
+static void jacobi_rot(double app, double aqq, double apq, double* cs, double* sn) {
+  if (apq == 0.0) {
+    *cs = 1.0;
+    *sn = 0.0;
+    return;
+  }
+  double theta = (aqq - app) / (2.0 * apq);
+  double t = (theta >= 0.0 ? 1.0 : -1.0) / (fabs(theta) + sqrt(theta * theta + 1.0));
+  *cs = 1.0 / sqrt(t * t + 1.0);
+  *sn = t * *cs;
+}
+
 static void jacobi4(double A[4][4], double V[4][4], double lam[4]) {
   for (int i = 0; i < 4; ++i)
     for (int j = 0; j < 4; ++j) V[i][j] = (i == j) ? 1.0 : 0.0;
@@ -36,30 +53,35 @@ static void jacobi4(double A[4][4], double V[4][4], double lam[4]) {
         if (i != j) off += A[i][j] * A[i][j];
       }
     if (off <= 1e-32 * tot || off == 0.0) break;
-    for (int p = 0; p < 3; ++p)
-      for (int q = p + 1; q < 4; ++q) {
-        double apq = A[p][q];
-        if (apq == 0.0) continue;
-        double theta = (A[q][q] - A[p][p]) / (2.0 * apq);
-        double t = (theta >= 0.0 ? 1.0 : -1.0) / (fabs(theta) + sqrt(theta * theta + 1.0));
-        double cs = 1.0 / sqrt(t * t + 1.0), sn = t * cs;
-        for (int k = 0; k < 4; ++k) {
-          double akp = A[k][p], akq = A[k][q];
-          A[k][p] = cs * akp - sn * akq;
-          A[k][q] = sn * akp + cs * akq;
-        }
-        for (int k = 0; k < 4; ++k) {
-          double apk = A[p][k], aqk = A[q][k];
-          A[p][k] = cs * apk - sn * aqk;
-          A[q][k] = sn * apk + cs * aqk;
-        }
-        A[p][q] = A[q][p] = 0.0;
-        for (int k = 0; k < 4; ++k) {
-          double vkp = V[k][p], vkq = V[k][q];
-          V[k][p] = cs * vkp - sn * vkq;
-          V[k][q] = sn * vkp + cs * vkq;
-        }
+    for (int r = 0; r < 3; ++r) {
+      int p1 = 0, q1 = r + 1, p2 = r == 0 ? 2 : 1, q2 = r == 2 ? 2 : 3;
+      double c1, s1, c2, s2;
+      jacobi_rot(A[p1][p1], A[q1][q1], A[p1][q1], &c1, &s1);
+      jacobi_rot(A[p2][p2], A[q2][q2], A[p2][q2], &c2, &s2);
+      for (int k = 0; k < 4; ++k) {
+        double a1 = A[k][p1], b1 = A[k][q1], a2 = A[k][p2], b2 = A[k][q2];
+        A[k][p1] = c1 * a1 - s1 * b1;
+        A[k][q1] = s1 * a1 + c1 * b1;
+        A[k][p2] = c2 * a2 - s2 * b2;
+        A[k][q2] = s2 * a2 + c2 * b2;
       }
+      for (int k = 0; k < 4; ++k) {
+        double a1 = A[p1][k], b1 = A[q1][k], a2 = A[p2][k], b2 = A[q2][k];
+        A[p1][k] = c1 * a1 - s1 * b1;
+        A[q1][k] = s1 * a1 + c1 * b1;
+        A[p2][k] = c2 * a2 - s2 * b2;
+        A[q2][k] = s2 * a2 + c2 * b2;
+      }
+      A[p1][q1] = A[q1][p1] = 0.0;
+      A[p2][q2] = A[q2][p2] = 0.0;
+      for (int k = 0; k < 4; ++k) {
+        double a1 = V[k][p1], b1 = V[k][q1], a2 = V[k][p2], b2 = V[k][q2];
+        V[k][p1] = c1 * a1 - s1 * b1;
+        V[k][q1] = s1 * a1 + c1 * b1;
+        V[k][p2] = c2 * a2 - s2 * b2;
+        V[k][q2] = s2 * a2 + c2 * b2;
+      }
+    }
   }
   for (int i = 0; i < 4; ++i) lam[i] = A[i][i];
 }

@@ -488,7 +488,27 @@ struct QgArgs {
 constexpr int QG_THREADS = 1024;  // 256 (c, b) quads per pass (the synthetic config: 1016 in 4 passes, not 16)
 constexpr int QG_SHARED = 16 * 3 + 4 + (QG_THREADS / 64) * 16 + 16 * 2;  // V, V^-1, 1/(lam_k - lam_l), lam,
                                                                           // wave partials, M, W
-__device__ void qgrad_body(const QgArgs& a, int draw, int tid, double* sh) {
+// The (c, b) item's dL/dP block G (row-major 4x4) for qgrad_body: by default
+// the draw's dL/dP row (every lane of the item's quad loads all 16).
+struct RowsG {
+  const double* rows;
+  __device__ __forceinline__ void operator()(int idx, int, double (&G)[16]) const {
+    const double2* g2 = reinterpret_cast<const double2*>(rows + (size_t)idx * 16);
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const double2 v = g2[u];
+      G[2 * u] = v.x;
+      G[2 * u + 1] = v.y;
+    }
+  }
+};
+template <typename GP>
+__device__ void qgrad_body(const QgArgs& a, int draw, int tid, double* sh, const GP& getG);
+__device__ __forceinline__ void qgrad_body(const QgArgs& a, int draw, int tid, double* sh) {
+  qgrad_body(a, draw, tid, sh, RowsG{a.grows + (size_t)draw * a.grows_stride});
+}
+template <typename GP>
+__device__ void qgrad_body(const QgArgs& a, int draw, int tid, double* sh, const GP& getG) {
   double* sV = sh;
   double* sVi = sh + 16;
   double* srinv = sh + 32;
@@ -518,7 +538,6 @@ __device__ void qgrad_body(const QgArgs& a, int draw, int tid, double* sh) {
   __syncthreads();
   const double* mdl = a.model + (size_t)draw * (10 + 2 * C);
   const double* bl = a.blens + (size_t)draw * B;
-  const double* rows = a.grows + (size_t)draw * a.grows_stride;
   // a quad of lanes per (c, b): lane k forms row k of H = V^T G V^-T and
   // accumulates row k of M (4 values); e^{lam_k t} comes from lane k
   const int k = tid & 3;
@@ -529,13 +548,7 @@ __device__ void qgrad_body(const QgArgs& a, int draw, int tid, double* sh) {
       const int c = idx / B, b = idx - c * B;
       const double t = mdl[10 + c] * bl[b];
       double G[16];
-      const double2* g2 = reinterpret_cast<const double2*>(rows + (size_t)idx * 16);
-#pragma unroll
-      for (int u = 0; u < 8; ++u) {
-        const double2 v = g2[u];
-        G[2 * u] = v.x;
-        G[2 * u + 1] = v.y;
-      }
+      getG(idx, k, G);
       const double Ek = exp(slam[k] * t);
       double E[4];
       E[0] = dpp_d<0x00>(Ek);
@@ -1270,9 +1283,29 @@ struct PmatArgs {
   int with_eig;  // pmat_kernel forms the draw's eigensystem itself (small batches: no eig launch)
 };
 
-// Cyclic Jacobi eigendecomposition of a symmetric 4x4 (A overwritten).
-// No FMA contraction here or in eig_record: the host (single-launch path) and
-// the device (eig_kernel) then round every operation alike -- the same bits.
+// Jacobi eigendecomposition of a symmetric 4x4 (A overwritten) in the
+// parallel ordering: each sweep is three rounds of two rotations on disjoint
+// index pairs -- {(0,1),(2,3)}, {(0,2),(1,3)}, {(0,3),(1,2)}.  A round's two
+// rotation parameters read entries the other rotation does not change, so
+// their chains (division, square root, division, square root, division: the
+// latency of the solve on one GPU thread) run side by side -- three chains
+// per sweep instead of six.  Then A <- J^T A J and V <- V J for the round's
+// combined rotation J.  No FMA contraction here or in eig_record, and every
+// operation in the C oracle's order (oracle/cpu_pruner.c jacobi4): the same
+// bits -- the gradients' agreement with the oracle at 10^5-10^6 sites rests
+// on it (an independent eigensolver moves dL/dP by ~1e-9 relative there).
+__host__ __device__ inline void jacobi_rot(double app, double aqq, double apq, double& cs, double& sn) {
+#pragma clang fp contract(off)
+  if (apq == 0.0) {  // the identity
+    cs = 1.0;
+    sn = 0.0;
+    return;
+  }
+  const double theta = (aqq - app) / (2.0 * apq);
+  const double t = (theta >= 0.0 ? 1.0 : -1.0) / (fabs(theta) + sqrt(theta * theta + 1.0));
+  cs = 1.0 / sqrt(t * t + 1.0);
+  sn = t * cs;
+}
 __host__ __device__ void jacobi4(double A[4][4], double V[4][4], double lam[4]) {
 #pragma clang fp contract(off)
   for (int i = 0; i < 4; ++i)
@@ -1286,44 +1319,47 @@ __host__ __device__ void jacobi4(double A[4][4], double V[4][4], double lam[4]) 
       }
     if (off <= 1e-32 * tot || off == 0.0) break;
 #pragma unroll
-    for (int p = 0; p < 3; ++p)
+    for (int r = 0; r < 3; ++r) {
+      const int p1 = 0, q1 = r + 1;                       // (0,1) (0,2) (0,3)
+      const int p2 = r == 0 ? 2 : 1, q2 = r == 2 ? 2 : 3;  // (2,3) (1,3) (1,2)
+      double c1, s1, c2, s2;
+      jacobi_rot(A[p1][p1], A[q1][q1], A[p1][q1], c1, s1);
+      jacobi_rot(A[p2][p2], A[q2][q2], A[p2][q2], c2, s2);
 #pragma unroll
-      for (int q = p + 1; q < 4; ++q) {
-        const double apq = A[p][q];
-        if (apq == 0.0) continue;
-        const double theta = (A[q][q] - A[p][p]) / (2.0 * apq);
-        const double t = (theta >= 0.0 ? 1.0 : -1.0) / (fabs(theta) + sqrt(theta * theta + 1.0));
-        const double cs = 1.0 / sqrt(t * t + 1.0);
-        const double sn = t * cs;
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {  // A <- A R   (columns p, q)
-          const double akp = A[k][p], akq = A[k][q];
-          A[k][p] = cs * akp - sn * akq;
-          A[k][q] = sn * akp + cs * akq;
-        }
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {  // A <- R^T A (rows p, q)
-          const double apk = A[p][k], aqk = A[q][k];
-          A[p][k] = cs * apk - sn * aqk;
-          A[q][k] = sn * apk + cs * aqk;
-        }
-        A[p][q] = A[q][p] = 0.0;
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {  // V <- V R
-          const double vkp = V[k][p], vkq = V[k][q];
-          V[k][p] = cs * vkp - sn * vkq;
-          V[k][q] = sn * vkp + cs * vkq;
-        }
+      for (int k = 0; k < 4; ++k) {  // A <- A J   (columns)
+        const double a1 = A[k][p1], b1 = A[k][q1], a2 = A[k][p2], b2 = A[k][q2];
+        A[k][p1] = c1 * a1 - s1 * b1;
+        A[k][q1] = s1 * a1 + c1 * b1;
+        A[k][p2] = c2 * a2 - s2 * b2;
+        A[k][q2] = s2 * a2 + c2 * b2;
       }
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {  // A <- J^T A (rows)
+        const double a1 = A[p1][k], b1 = A[q1][k], a2 = A[p2][k], b2 = A[q2][k];
+        A[p1][k] = c1 * a1 - s1 * b1;
+        A[q1][k] = s1 * a1 + c1 * b1;
+        A[p2][k] = c2 * a2 - s2 * b2;
+        A[q2][k] = s2 * a2 + c2 * b2;
+      }
+      A[p1][q1] = A[q1][p1] = 0.0;
+      A[p2][q2] = A[q2][p2] = 0.0;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {  // V <- V J
+        const double a1 = V[k][p1], b1 = V[k][q1], a2 = V[k][p2], b2 = V[k][q2];
+        V[k][p1] = c1 * a1 - s1 * b1;
+        V[k][q1] = s1 * a1 + c1 * b1;
+        V[k][p2] = c2 * a2 - s2 * b2;
+        V[k][q2] = s2 * a2 + c2 * b2;
+      }
+    }
   }
   for (int i = 0; i < 4; ++i) lam[i] = A[i][i];
 }
 
 // Normalised Q and its eigensystem of one draw's model vector (the
-// EIG_LEN record: P(t) = m1 diag(exp(lam t)) m2, Q, the normaliser).  Host
-// and device share it: eig_kernel runs it one thread per draw for batched
-// device-buffer evaluations, the single-launch small-batch path on the host
-// (a 4x4 Jacobi is a serial chain: ~12 us as one GPU thread, ~1 us here).
+// EIG_LEN record: P(t) = m1 diag(exp(lam t)) m2, Q, the normaliser):
+// eig_kernel runs it one thread per draw for batches, lane 0 of each pmat
+// wave for small ones (a serial chain of one thread either way).
 __host__ __device__ void eig_record(const double* mdl, int kind, double* out) {
 #pragma clang fp contract(off)
   if (kind == PHY_JC69) {  // generate_script.py:765-769 (closed form; Q for dP/dt only)
@@ -1496,6 +1532,62 @@ __global__ void __launch_bounds__(256) gsum_kernel(FinArgs a) {
 //           over slots + a fixed-shape wave reduction;
 //   chain rule  dlogL/dt_{b,c} = <G_bc, Q P_bc>,  dlogL/db = sum_c r_c (.),
 //           dlogL/dr_c = sum_b b (.)   (generate_script.py:663-671 blens).
+// The fused epilogue's dL/dP provider (finalize_kernel with the chain rule):
+// lane k of the (c, b) item's quad forms row k of G -- the sum of the gx
+// workgroup slots (gsum_in; written out as the dL/dP row) or the row
+// itself -- then the quad shares its rows by DPP, and its share of <G, Q P>
+// goes to inner[idx] after a quad sum.  One pass over the items instead of
+// slot sums -> HBM -> <G, QP> -> HBM -> the chain rule's reads.
+struct FusedG {
+  const FinArgs& a;
+  int draw;
+  double* inner;    // LDS [C*B]
+  const double* Q;  // LDS [16]
+  __device__ __forceinline__ void operator()(int idx, int k, double (&G)[16]) const {
+    const int C = a.C, B = a.B;
+    const int c = idx / B, b = idx - c * B;
+    const int mm = a.gpos[b];
+    double* grow = a.grows + (size_t)draw * a.grows_stride + (size_t)idx * 16 + k * 4;
+    double r[4];
+    if (a.gsum_in) {
+      const size_t per_wg = (size_t)C * a.nmat * 16;
+      const double* src = a.gslot + (size_t)draw * a.gx * per_wg + ((size_t)c * a.nmat + mm) * 16 + k * 4;
+      double2 lo = *reinterpret_cast<const double2*>(src), hi = *reinterpret_cast<const double2*>(src + 2);
+      r[0] = lo.x; r[1] = lo.y; r[2] = hi.x; r[3] = hi.y;
+      for (int w = 1; w < a.gx; ++w) {
+        lo = *reinterpret_cast<const double2*>(src + (size_t)w * per_wg);
+        hi = *reinterpret_cast<const double2*>(src + (size_t)w * per_wg + 2);
+        r[0] += lo.x; r[1] += lo.y; r[2] += hi.x; r[3] += hi.y;
+      }
+      *reinterpret_cast<double2*>(grow) = make_double2(r[0], r[1]);
+      *reinterpret_cast<double2*>(grow + 2) = make_double2(r[2], r[3]);
+    } else {
+      const double2 lo = *reinterpret_cast<const double2*>(grow), hi = *reinterpret_cast<const double2*>(grow + 2);
+      r[0] = lo.x; r[1] = lo.y; r[2] = hi.x; r[3] = hi.y;
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      G[j] = dpp_d<0x00>(r[j]);
+      G[4 + j] = dpp_d<0x55>(r[j]);
+      G[8 + j] = dpp_d<0xAA>(r[j]);
+      G[12 + j] = dpp_d<0xFF>(r[j]);
+    }
+    // row k of <G, Q P>: sum_j G[k][j] (Q P)[k][j]; P column-major in its record
+    const double* P = a.pmat + ((size_t)draw * C * a.nmat + (size_t)c * a.nmat + mm) * a.R * 4;
+    double sv = 0.0;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const double2 p01 = *reinterpret_cast<const double2*>(P + j * 4);
+      const double2 p23 = *reinterpret_cast<const double2*>(P + j * 4 + 2);
+      const double qp = fma(Q[k * 4 + 3], p23.y, fma(Q[k * 4 + 2], p23.x, fma(Q[k * 4 + 1], p01.y, Q[k * 4] * p01.x)));
+      sv = fma(r[j], qp, sv);
+    }
+    sv += dpp_d<0xB1>(sv);  // quad_perm [1,0,3,2]
+    sv += dpp_d<0x4E>(sv);  // quad_perm [2,3,0,1]
+    if (k == 0) inner[idx] = sv;
+  }
+};
+
 __global__ void __launch_bounds__(1024) finalize_kernel(FinArgs a) {
   extern __shared__ double fsh[];  // inner[C*B], Q[16]
   const int draw = blockIdx.x;
@@ -1504,7 +1596,9 @@ __global__ void __launch_bounds__(1024) finalize_kernel(FinArgs a) {
   double* Q = fsh + (size_t)C * B;
   double* out = a.out + (size_t)draw * a.outlen;
   const size_t wg0 = (size_t)draw * a.gx;
-  if (a.gsum_in) {
+  // the chain rule's pass also sums the slots and forms <G, QP> (FusedG)
+  const bool fused = a.qf && !a.g_direct && a.kind != PHY_JC69 && blockDim.x == QG_THREADS;
+  if (a.gsum_in && !fused) {
     // the draw's dL/dP rows from its gx workgroup slots, summed in slot
     // order (gsum_kernel's work, for draws spread over a few workgroups);
     // made visible to the workgroup by the barriers below
@@ -1567,9 +1661,14 @@ __global__ void __launch_bounds__(1024) finalize_kernel(FinArgs a) {
     }
   }
   __syncthreads();  // dL/dP rows and Q visible to the whole workgroup
+  if (fused) {
+    const QgArgs q{a.eig, a.model, a.blens, a.grows, a.grows_stride, a.out, a.outlen, C, B, a.kind};
+    qgrad_body(q, draw, threadIdx.x, fsh + (size_t)C * B + 16 + blockDim.x, FusedG{a, draw, inner, Q});
+    __syncthreads();  // inner[] complete (and the chain rule's tail done)
+  }
   const int rec = a.R * 4;
   const double* pm = a.pmat + (size_t)draw * C * a.nmat * rec;
-  for (int idx = threadIdx.x; idx < C * B; idx += blockDim.x) {
+  for (int idx = threadIdx.x; idx < C * B && !fused; idx += blockDim.x) {
     if (a.g_direct) {  // formed by the sweep's last flush
       inner[idx] = a.inner[(size_t)draw * C * B + idx];
       continue;
@@ -1595,7 +1694,7 @@ __global__ void __launch_bounds__(1024) finalize_kernel(FinArgs a) {
       }
     inner[idx] = s;  // dlogL / dt_{b,c}
   }
-  __syncthreads();
+  if (!fused) __syncthreads();
   const double* rs = a.model + (size_t)draw * (10 + 2 * C) + 10;
   const double* bl = a.blens + (size_t)draw * B;
   for (int b = threadIdx.x; b < B; b += blockDim.x) {
@@ -1608,7 +1707,7 @@ __global__ void __launch_bounds__(1024) finalize_kernel(FinArgs a) {
     for (int b = 0; b < B; ++b) s = fma(bl[b], inner[c * B + b], s);
     out[1 + B + c] = s;
   }
-  if (a.qf) {  // the Q-parameter chain rule (qgrad_kernel's work, same bits)
+  if (a.qf && !fused) {  // the Q-parameter chain rule (qgrad_kernel's work, same bits)
     __syncthreads();  // the finalize's root term visible to thread 0 of qgrad_body
     const QgArgs q{a.eig, a.model, a.blens, a.grows, a.grows_stride, a.out, a.outlen, C, B, a.kind};
     qgrad_body(q, draw, threadIdx.x, fsh + (size_t)C * B + 16 + blockDim.x);

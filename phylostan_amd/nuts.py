@@ -39,7 +39,10 @@ class _Point:
         self.q, self.p, self.lp, self.g = q, p, lp, g
 
     def copy(self):
-        return _Point(self.q.copy(), self.p.copy(), self.lp, self.g.copy())
+        # shallow: the sampler never changes a position, momentum or gradient
+        # array in place (every update binds a new array), so a snapshot can
+        # share them
+        return _Point(self.q, self.p, self.lp, self.g)
 
 
 class Chain:
@@ -188,7 +191,7 @@ class Chain:
 
     @staticmethod
     def _criterion(ps_minus, ps_plus, rho):
-        return float(np.dot(ps_plus, rho)) > 0 and float(np.dot(ps_minus, rho)) > 0
+        return ps_plus.dot(rho) > 0 and ps_minus.dot(rho) > 0
 
     def _build_tree(self, depth, z, H0, sign, st):
         """Returns (valid, z_propose, p_sharp_beg, p_sharp_end, rho, p_beg,
@@ -205,7 +208,7 @@ class Chain:
             lsw = H0 - h if h != math.inf else -math.inf
             st["sum_metro_prob"] += 1.0 if H0 - h > 0 else math.exp(H0 - h)
             ps = self.inv_metric * z.p
-            return (not st["divergent"], z.copy(), ps, ps.copy(), z.p.copy(), z.p.copy(), z.p.copy(), lsw)
+            return (not st["divergent"], z.copy(), ps, ps, z.p, z.p, z.p, lsw)
         v1, zp, ps_beg, ps_init_end, rho_init, p_beg, p_init_end, lsw_init = \
             yield from self._build_tree(depth - 1, z, H0, sign, st)
         if not v1:
@@ -232,11 +235,8 @@ class Chain:
         H0 = self._H(z)
         z_fwd, z_bck, z_sample = z.copy(), z.copy(), z.copy()
         ps0 = self.inv_metric * z.p
-        p_fwd_fwd = z.p.copy(); ps_fwd_fwd = ps0.copy()
-        p_fwd_bck = z.p.copy(); ps_fwd_bck = ps0.copy()
-        p_bck_fwd = z.p.copy(); ps_bck_fwd = ps0.copy()
-        p_bck_bck = z.p.copy(); ps_bck_bck = ps0.copy()
-        rho = z.p.copy()
+        p_fwd_fwd = p_fwd_bck = p_bck_fwd = p_bck_bck = rho = z.p
+        ps_fwd_fwd = ps_fwd_bck = ps_bck_fwd = ps_bck_bck = ps0
         lsw = 0.0
         st = {"n_leapfrog": 0, "sum_metro_prob": 0.0, "divergent": False}
         depth = 0
