@@ -663,7 +663,7 @@ __device__ void qgrad_body(const QgArgs& a, int draw, int tid, double* sh, const
 #define PHY_WPE2 2  // waves per SIMD the K=2 kernel is register-budgeted for
 #endif
 template <int MAXT, int K, bool DL>
-__global__ void __launch_bounds__(MAXT) __attribute__((amdgpu_waves_per_eu(K == 2 ? PHY_WPE2 : 4)))
+__global__ void __launch_bounds__(MAXT) __attribute__((amdgpu_waves_per_eu(MAXT <= 512 ? PHY_WPE2 : 4)))
     sweep_kernel(SweepArgs a, const int* __restrict__ prog) {
   extern __shared__ __attribute__((aligned(16))) unsigned char lds_raw[];
   const int lane = threadIdx.x & (WAVE - 1);
@@ -1742,6 +1742,8 @@ struct phy_ctx {
   int wg_budget, cols_pref, wg_cap, lds_budget;
   int cu_count = 256, wg_resident = 512;  // resident workgroups of the current plan
   int K = 1;                   // columns per lane of the current plan
+  bool klat = false;           // K = 1 latency plan (sweep_kernel<512, 1, .>: no register spills)
+  bool klat_pref = true;       // PHY_KLAT=0: the latency plan keeps the four-wave K = 1 kernel
   bool qfuse_pref = true;      // Q-parameter chain rule inside the sweep (PHY_QFUSE=0: off)
   int cap_m = 0, nchunks = 0;  // current LDS plan
   int deep_pref = 0;           // deep stack: 0 automatic, 1 LDS, 2 global
@@ -1773,6 +1775,7 @@ struct phy_ctx {
   int* d_mat_branch = nullptr;
   double* d_pmat = nullptr;
   double* d_eig = nullptr;
+  const double* eig_cur = nullptr;  // the eigensystems of the launch in flight: d_eig, or host-formed rows in d_in
   double* d_inner = nullptr;
   double* d_model = nullptr;
   double* d_blens = nullptr;
@@ -1780,10 +1783,11 @@ struct phy_ctx {
   double* d_site = nullptr;
   // small host-buffer evaluations (phy_eval with n <= PIN_DRAWS): inputs packed
   // into one pinned staging buffer and one device buffer (one H2D copy), the
-  // output rows back through pinned memory (asynchronous DMA both ways)
-  double* h_in = nullptr;   // pinned [PIN_DRAWS][B + model_len]
+  // output rows back through pinned memory (asynchronous DMA both ways); the
+  // draws' eigensystems are formed on the host (stage_small) and ride along
+  double* h_in = nullptr;   // pinned [PIN_DRAWS][B + model_len + EIG_LEN]
   double* h_out = nullptr;  // pinned [PIN_DRAWS][full output row]
-  double* d_in = nullptr;   // device [PIN_DRAWS][B + model_len]
+  double* d_in = nullptr;   // device [PIN_DRAWS][B + model_len + EIG_LEN]
   int pending = 0;          // draws of a phy_eval_submit not yet collected by phy_eval_wait
   double2* d_scratch = nullptr;
   double2* d_dstk = nullptr;
@@ -2030,12 +2034,17 @@ constexpr int MIN_CAP = 24;  // an occupancy level is taken only if chunks stay 
 
 int nblk_for(int P, int K) { return (P + WAVE * K - 1) / (WAVE * K); }
 // The sweep instantiation of a plan: K columns per lane, deep stack in LDS.
-const void* sweep_kernel_ptr(int K, bool dl) {
+// K = 1 has two register budgets: four waves per SIMD (1,024-thread
+// workgroups, 128 VGPRs: spills) for wide launches with C > 8, and the
+// sampler's latency plan (a few draws: at most one wave per SIMD is busy)
+// at 256 VGPRs without spills (lat).
+const void* sweep_kernel_ptr(int K, bool dl, bool lat) {
   if (K == 2) return dl ? (const void*)sweep_kernel<512, 2, true> : (const void*)sweep_kernel<512, 2, false>;
+  if (lat) return dl ? (const void*)sweep_kernel<512, 1, true> : (const void*)sweep_kernel<512, 1, false>;
   return dl ? (const void*)sweep_kernel<1024, 1, true> : (const void*)sweep_kernel<1024, 1, false>;
 }
 int alloc_wg_buffers(phy_ctx* c, long cap);
-int waves_per_simd(int K) { return K == 2 ? PHY_WPE2 : 4; }  // the kernel's register budget
+int waves_per_simd(int K, bool lat) { return (K == 2 || lat) ? PHY_WPE2 : 4; }  // the kernel's register budget
 
 // Columns per lane, matrices per LDS chunk and the chunk boundaries over the
 // program.  Occupancy is bounded by registers (two waves per SIMD for K=2,
@@ -2050,9 +2059,13 @@ int plan_chunks(phy_ctx* c) {
   // step body (fluA, 4 draws: 182 -> 167 us per call; 100 draws: K = 2 stays
   // ahead, 220 against 235 us)
   int K = c->cols_pref;
+  bool lat = false;
   if (!K) {
     K = c->C <= 8 ? 2 : 1;
-    if (K == 2 && (long)c->max_draws * nblk_for(c->P, 1) * c->C <= 4L * c->cu_count) K = 1;
+    if (K == 2 && (long)c->max_draws * nblk_for(c->P, 1) * c->C <= 4L * c->cu_count) {
+      K = 1;
+      lat = c->klat_pref;
+    }
   }
   if (K == 2 && c->C > 8) return fail(PHY_EINVAL, "two columns per lane need C <= 8");
   if ((size_t)std::max(c->nslots, c->ndeep) * K * 2 * c->C * WAVE * 16 >= (size_t)OOB)
@@ -2067,7 +2080,7 @@ int plan_chunks(phy_ctx* c) {
   auto fits = [&](int cap, size_t budget) {
     return lds_bytes(c->S, c->C, c->R, cap, K, ndl) <= budget && cap >= std::min(c->nmat, MIN_CAP);
   };
-  const int by_waves = std::max(1, 4 * waves_per_simd(K) / c->C);  // workgroups per CU
+  const int by_waves = std::max(1, 4 * waves_per_simd(K, lat) / c->C);  // workgroups per CU
   int cap = 0;
   // Deep-stack placement at a given LDS share: the whole stack in LDS if it
   // fits beside chunks of MIN_CAP matrices (mode 0/1), else (mode 0/2) its
@@ -2099,6 +2112,7 @@ int plan_chunks(phy_ctx* c) {
   const size_t lds = lds_bytes(c->S, c->C, c->R, cap, K, ndl);
   if (lds > LDS_CAP) return fail(PHY_EINVAL, "tree too large for LDS (tips of one block)");
   c->K = K;
+  c->klat = lat;
   c->nblk = nb;
   ++c->plan_gen;
   c->wg_resident = c->cu_count * std::min<int>(by_waves, (int)(LDS_CAP / lds));
@@ -2311,7 +2325,7 @@ int launch_class(phy_ctx* ctx, int n, const double* d_blens, const double* d_mod
   if (d_site)
     hipLaunchKernelGGL(cls_site_kernel, dim3((ctx->P + 255) / 256, n), dim3(256), 0, st,
                        (const double*)e->d_sitecls, (const int*)e->d_pat_root, d_site, ctx->P, e->nroot);
-  FinArgs fa{ctx->d_gslot, e->d_sslot, ctx->d_pmat, ctx->d_eig, d_blens, d_model, ctx->d_gpos, ctx->d_inner, d_out,
+  FinArgs fa{ctx->d_gslot, e->d_sslot, ctx->d_pmat, ctx->eig_cur, d_blens, d_model, ctx->d_gpos, ctx->d_inner, d_out,
              C,            B,          ctx->nmat,   e->nrootch,  phy_output_len(ctx), 0, ctx->R, grows, gstride,
              ctx->kind,    0,          ctx->qfuse_pref ? 1 : 0};
   launch_finalize(fa, n, st);
@@ -2349,7 +2363,7 @@ int launch_res(phy_ctx* ctx, int n, const double* d_blens, const double* d_model
   if (d_site)
     hipLaunchKernelGGL(cls_site_kernel, dim3((ctx->P + 255) / 256, n), dim3(256), 0, st,
                        (const double*)e->d_sitecls, (const int*)e->d_pat_root, d_site, ctx->P, e->nroot);
-  FinArgs fa{ctx->d_gslot, e->d_sslot, ctx->d_pmat, ctx->d_eig, d_blens, d_model, ctx->d_gpos, ctx->d_inner, d_out,
+  FinArgs fa{ctx->d_gslot, e->d_sslot, ctx->d_pmat, ctx->eig_cur, d_blens, d_model, ctx->d_gpos, ctx->d_inner, d_out,
              C,            B,          ctx->nmat,   1,           phy_output_len(ctx), 0, ctx->R, grows, gstride,
              ctx->kind,    0,          ctx->qfuse_pref ? 1 : 0};
   launch_finalize(fa, n, st);
@@ -2358,15 +2372,17 @@ int launch_res(phy_ctx* ctx, int n, const double* d_blens, const double* d_model
 }
 
 int launch(phy_ctx* ctx, int n, const double* d_blens, const double* d_model, double* d_out,
-           double* d_site, hipStream_t st) {
+           double* d_site, hipStream_t st, const double* d_eig_in = nullptr) {
   const int C = ctx->C, B = ctx->B;
+  ctx->eig_cur = d_eig_in ? d_eig_in : ctx->d_eig;
   {
-    // small batches: each pmat wave forms its draw's eigensystem (one launch
-    // less on the sampler's path); large ones: one thread per draw first
-    const int with_eig = n <= EIG_FUSE_MAX ? 1 : 0;
-    PmatArgs pa{d_model, d_blens, ctx->d_mat_branch, ctx->d_eig, ctx->d_pmat, C, B, ctx->kind, ctx->nmat, n,
-                ctx->R, ctx->extra, with_eig};
-    if (!with_eig) {
+    // eigensystems: given (host-formed, the small host-buffer path); small
+    // device batches: each pmat wave forms its draw's (one launch less);
+    // large ones: one thread per draw first
+    const int with_eig = (!d_eig_in && n <= EIG_FUSE_MAX) ? 1 : 0;
+    PmatArgs pa{d_model, d_blens, ctx->d_mat_branch, const_cast<double*>(ctx->eig_cur), ctx->d_pmat, C, B, ctx->kind,
+                ctx->nmat, n, ctx->R, ctx->extra, with_eig};
+    if (!with_eig && !d_eig_in) {
       hipLaunchKernelGGL(eig_kernel, dim3((n + 63) / 64), dim3(64), 0, st, pa);
       HIP_TRY(hipGetLastError());
     }
@@ -2384,7 +2400,7 @@ int launch(phy_ctx* ctx, int n, const double* d_blens, const double* d_model, do
                                : launch_pattern(ctx, n, d_blens, d_model, d_out, d_site, st, grows, gstride, &qdone);
   if (rc0) return rc0;
   if (!qdone) {
-    FinArgs qa{ctx->d_gslot, ctx->d_sslot, ctx->d_pmat, ctx->d_eig, d_blens, d_model, ctx->d_gpos, ctx->d_inner,
+    FinArgs qa{ctx->d_gslot, ctx->d_sslot, ctx->d_pmat, ctx->eig_cur, d_blens, d_model, ctx->d_gpos, ctx->d_inner,
                d_out,        C,            B,           ctx->nmat,   1,       phy_output_len(ctx), 0, ctx->R, grows,
                gstride,      ctx->kind};
     hipLaunchKernelGGL(qgrad_kernel, dim3(n), dim3(QG_THREADS), 0, st, qa);
@@ -2482,7 +2498,7 @@ int launch_pattern(phy_ctx* ctx, int n, const double* d_blens, const double* d_m
   const int fin = (g_direct && ctx->fin_pref && ((size_t)C * B + 8 * C) * 8 <= room) ? 1 : 0;
   const int qf = (fin && ctx->qfuse_pref && ((size_t)C * B + 8 * C + QG_SHARED) * 8 <= room) ? 1 : 0;
   SweepArgs sa{ctx->d_tips,  ctx->d_w,     ctx->d_pmat,  d_model,      ctx->d_scratch, ctx->d_dstk,
-               ctx->d_gslot, ctx->d_sslot, d_site,       d_out,        ctx->d_mat_branch, ctx->d_eig,
+               ctx->d_gslot, ctx->d_sslot, d_site,       d_out,        ctx->d_mat_branch, ctx->eig_cur,
                ctx->d_inner, ctx->S,       ctx->P,       ctx->Ppad,    C,              ctx->nsteps,
                ctx->nslots,  ctx->ndeep,   ctx->ndl,     ctx->nblk,    ctx->nmat,    ctx->R,         ctx->cap_m,
                B,            phy_output_len(ctx), g_direct, ctx->extra, fin, d_blens, grows, gstride,
@@ -2493,7 +2509,7 @@ int launch_pattern(phy_ctx* ctx, int n, const double* d_blens, const double* d_m
     if (rc) return rc;
   }
   const int threads = C * WAVE;
-  const void* kern = sweep_kernel_ptr(ctx->K, ctx->deep_lds);
+  const void* kern = sweep_kernel_ptr(ctx->K, ctx->deep_lds, ctx->klat);
   {
     const int* prog = ctx->d_prog;
     void* kargs[] = {(void*)&sa, (void*)&prog};
@@ -2505,7 +2521,7 @@ int launch_pattern(phy_ctx* ctx, int n, const double* d_blens, const double* d_m
   // (one epilogue launch: slot sums, finalize, chain rule); over many, the
   // wide gsum kernel first
   const int gsum_in = (!g_direct && gx <= 16) ? 1 : 0;
-  FinArgs fa{ctx->d_gslot, ctx->d_sslot, ctx->d_pmat, ctx->d_eig, d_blens, d_model, ctx->d_gpos, ctx->d_inner, d_out,
+  FinArgs fa{ctx->d_gslot, ctx->d_sslot, ctx->d_pmat, ctx->eig_cur, d_blens, d_model, ctx->d_gpos, ctx->d_inner, d_out,
              C,            B,            ctx->nmat,   gx,          phy_output_len(ctx), g_direct, ctx->R, grows, gstride,
              ctx->kind,    gsum_in,      (!fin && ctx->qfuse_pref) ? 1 : 0};
   if (!g_direct && !gsum_in) {
@@ -2548,6 +2564,22 @@ int alloc_wg_buffers(phy_ctx* c, long cap) {
   c->d_gslot = gsl;
   c->d_sslot = ssl;
   return PHY_OK;
+}
+
+// The small host-buffer path's staging: blens, model vectors and the draws'
+// eigensystems (eig_record on the host: the same operations in the same
+// order as eig_kernel and the C oracle, with no FMA contraction, so the same
+// bits; formed on the device by one lane per pmat wave they took 13 us of a
+// 4-draw fluA call -- a serial chain of divisions and square roots) packed
+// for one H2D copy.  Returns the doubles to copy.
+size_t stage_small(phy_ctx* ctx, int n, const double* blens, const double* model) {
+  const int ml = 10 + 2 * ctx->C;
+  const size_t nb = (size_t)n * ctx->B, nm = (size_t)n * ml;
+  std::memcpy(ctx->h_in, blens, sizeof(double) * nb);
+  std::memcpy(ctx->h_in + nb, model, sizeof(double) * nm);
+  double* eg = ctx->h_in + nb + nm;
+  for (int d = 0; d < n; ++d) eig_record(model + (size_t)d * ml, ctx->kind, eg + (size_t)d * EIG_LEN);
+  return nb + nm + (size_t)n * EIG_LEN;
 }
 
 }  // namespace
@@ -2634,6 +2666,8 @@ int phy_create(int S, int P, int C, int rooted, int model, const uint8_t* tipcod
     c->qfuse_pref = qk ? atoi(qk) != 0 : true;
     const char* gk = getenv("PHY_GRAPH");
     c->graph_pref = gk ? atoi(gk) != 0 : false;
+    const char* lk = getenv("PHY_KLAT");
+    c->klat_pref = lk ? atoi(lk) != 0 : true;
 
   }
   hipError_t he = hipSetDevice(device);
@@ -2652,9 +2686,9 @@ int phy_create(int S, int P, int C, int rooted, int model, const uint8_t* tipcod
   // gfx950: one workgroup may use the whole 160 KiB LDS; dynamic LDS above
   // 64 KiB has to be opted into per kernel.
   {
-    for (int k = 0; k < 4; ++k)
-      (void)hipFuncSetAttribute(sweep_kernel_ptr(1 + (k & 1), (k >> 1) & 1), hipFuncAttributeMaxDynamicSharedMemorySize,
-                                (int)LDS_CAP);
+    for (int k = 0; k < 8; ++k)
+      (void)hipFuncSetAttribute(sweep_kernel_ptr(1 + (k & 1), (k >> 1) & 1, (k >> 2) & 1),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)LDS_CAP);
     (void)hipFuncSetAttribute((const void*)res_fwd_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)LDS_CAP);
     (void)hipFuncSetAttribute((const void*)res_rev_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)LDS_CAP);
   }
@@ -2698,8 +2732,8 @@ int phy_create(int S, int P, int C, int rooted, int model, const uint8_t* tipcod
   {
     const size_t pin = (size_t)std::min(max_draws, PIN_DRAWS);
     const size_t outlen_full = (size_t)1 + c->B + 2 * C + 14 + (size_t)16 * C * c->B;
-    TRY_C(dalloc(&c->d_in, pin * (c->B + 10 + 2 * C)));
-    HIP_C(hipHostMalloc((void**)&c->h_in, sizeof(double) * pin * (c->B + 10 + 2 * C), hipHostMallocDefault));
+    TRY_C(dalloc(&c->d_in, pin * (c->B + 10 + 2 * C + EIG_LEN)));
+    HIP_C(hipHostMalloc((void**)&c->h_in, sizeof(double) * pin * (c->B + 10 + 2 * C + EIG_LEN), hipHostMallocDefault));
     HIP_C(hipHostMalloc((void**)&c->h_out, sizeof(double) * pin * outlen_full, hipHostMallocDefault));
   }
   {
@@ -2909,11 +2943,10 @@ int phy_eval_submit(phy_ctx* ctx, int n_draws, const double* blens, const double
   const int ml = 10 + 2 * ctx->C;
   const size_t nb = (size_t)n_draws * ctx->B, nm = (size_t)n_draws * ml;
   const size_t no = (size_t)n_draws * phy_output_len(ctx);
-  std::memcpy(ctx->h_in, blens, sizeof(double) * nb);
-  std::memcpy(ctx->h_in + nb, model, sizeof(double) * nm);
+  const size_t nin = stage_small(ctx, n_draws, blens, model);
   int rc = launch_graphed(ctx, n_draws, ctx->h_in, ctx->d_in, ctx->h_out, nullptr, st, [&]() -> int {
-    HIP_TRY(hipMemcpyAsync(ctx->d_in, ctx->h_in, sizeof(double) * (nb + nm), hipMemcpyHostToDevice, st));
-    int r = launch(ctx, n_draws, ctx->d_in, ctx->d_in + nb, ctx->d_out, nullptr, st);
+    HIP_TRY(hipMemcpyAsync(ctx->d_in, ctx->h_in, sizeof(double) * nin, hipMemcpyHostToDevice, st));
+    int r = launch(ctx, n_draws, ctx->d_in, ctx->d_in + nb, ctx->d_out, nullptr, st, ctx->d_in + nb + nm);
     if (r) return r;
     HIP_TRY(hipMemcpyAsync(ctx->h_out, ctx->d_out, sizeof(double) * no, hipMemcpyDeviceToHost, st));
     return PHY_OK;
@@ -2955,12 +2988,11 @@ int phy_eval(phy_ctx* ctx, int n_draws, const double* blens, const double* model
   if (n_draws <= PIN_DRAWS && ctx->h_in && ctx->h_out && ctx->d_in) {  // the small-batch (sampler) path
     const size_t nb = (size_t)n_draws * ctx->B, nm = (size_t)n_draws * ml;
     const size_t no = (size_t)n_draws * phy_output_len(ctx);
-    std::memcpy(ctx->h_in, blens, sizeof(double) * nb);
-    std::memcpy(ctx->h_in + nb, model, sizeof(double) * nm);
+    const size_t nin = stage_small(ctx, n_draws, blens, model);
     double* dsite = site_ll ? ctx->d_site : nullptr;
     int rc = launch_graphed(ctx, n_draws, ctx->h_in, ctx->d_in, ctx->h_out, dsite, st, [&]() -> int {
-      HIP_TRY(hipMemcpyAsync(ctx->d_in, ctx->h_in, sizeof(double) * (nb + nm), hipMemcpyHostToDevice, st));
-      int r = launch(ctx, n_draws, ctx->d_in, ctx->d_in + nb, ctx->d_out, dsite, st);
+      HIP_TRY(hipMemcpyAsync(ctx->d_in, ctx->h_in, sizeof(double) * nin, hipMemcpyHostToDevice, st));
+      int r = launch(ctx, n_draws, ctx->d_in, ctx->d_in + nb, ctx->d_out, dsite, st, ctx->d_in + nb + nm);
       if (r) return r;
       HIP_TRY(hipMemcpyAsync(ctx->h_out, ctx->d_out, sizeof(double) * no, hipMemcpyDeviceToHost, st));
       return PHY_OK;
