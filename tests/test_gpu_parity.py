@@ -8,6 +8,7 @@ reference; we hold the HIP path to far tighter):
 """
 import numpy as np
 import pytest
+import torch  # noqa: F401 -- torch's own HIP runtime must load before the engine's
 
 from tests import cases
 
@@ -243,6 +244,37 @@ def test_nonfinite_is_minus_inf():
     mv[10 + case.C:] = 0.0  # ps = 0 -> L = 0 -> log L = -inf
     res = eng.evaluate(case.blens, mv)
     assert res.loglik == -np.inf
+
+
+@pytest.mark.parametrize("make,n", [(cases.hcv_case, 5), (cases.fluA_case, 3), (cases.hcv_case, 40)],
+                         ids=["HCV-5", "fluA-3", "HCV-40"])
+def test_host_eigensystems_bitwise_equal_device(make, n):
+    """The small host-buffer path forms the draws' eigensystems on the host
+    (stage_small); the device path forms them on the GPU -- inside the pmat
+    waves for <= 32 draws, in eig_kernel above.  Same operations in the same
+    order without FMA contraction: every output row bit for bit."""
+    base = make()
+    rng = np.random.default_rng(29)
+    from phylostan_amd import models
+    eng = _engine(base, max_draws=n)
+    bl = base.blens[None, :] * rng.uniform(0.6, 1.4, (n, base.blens.size))
+    mv = []
+    for _ in range(n):
+        f = rng.dirichlet([20.0] * 4)
+        r = (models.hky_exchangeabilities(rng.uniform(2.0, 9.0)) if base.model == "HKY"
+             else base.rates * rng.uniform(0.6, 1.4, 6))
+        rs, ps = models.weibull_site_rates(rng.uniform(0.2, 2.0), base.C)
+        mv.append(models.model_vector(f, r, rs, ps))
+    mv = np.array(mv)
+    host = eng.evaluate_rows(bl, mv)
+    d_bl = torch.tensor(bl, device="cuda:0")
+    d_mv = torch.tensor(mv, device="cuda:0")
+    d_out = torch.zeros((n, eng.outlen), dtype=torch.float64, device="cuda:0")
+    stream = torch.cuda.current_stream().cuda_stream
+    eng.evaluate_device(d_bl.data_ptr(), d_mv.data_ptr(), d_out.data_ptr(), 0, n_draws=n, stream=stream)
+    torch.cuda.synchronize()
+    dev = d_out.cpu().numpy()
+    assert np.array_equal(host, dev), "max |diff| %.3e" % np.max(np.abs(host - dev))
 
 
 def test_submit_wait_equals_eval_and_guards_in_flight():
