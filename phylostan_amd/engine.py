@@ -246,8 +246,9 @@ class TreeLikelihood:
         """For host-driven samplers (a few draws per call, one call per
         leapfrog / ELBO round): the resident class sweep when the tree is
         rooted and its class state fits in LDS -- lower latency per small
-        batch (fluA 4 draws 185 us against 197 us per call, HCV 131 against
-        194) -- else the automatic engine.  Returns the name."""
+        batch (round 3, one box: fluA 4 draws 135 us against 139-141 us per
+        call, HCV 97-103 against 132-135) -- else the automatic
+        engine.  Returns the name."""
         try:
             self.set_engine("resident")
         except _lib.PhyloHipError:
