@@ -61,9 +61,9 @@ def parse():
                          "state in LDS) or the context's automatic choice")
     ap.add_argument("--json-out", default=None)
     ap.add_argument("--shard-of", type=int, default=0,
-                    help="synthetic: evaluate only the first of this many pattern shards on one GPU, with no "
-                         "collective -- what each rank of an N-GPU run computes (a projection, not the "
-                         "headline)")
+                    help="evaluate only the first of this many pattern shards on one GPU, with no collective -- "
+                         "what each rank of a site-sharded N-GPU run computes (a projection, not the headline; "
+                         "for the batched workloads, SURVEY 8e's site sharding beside the replicas)")
     ap.add_argument("--dry-run", action="store_true",
                     help="launcher check only: ranks join a gloo group on the CPU, all-reduce their rank "
                          "ids and exit (no GPU, no evaluation)")
@@ -315,6 +315,10 @@ def main():
         prob = BATCHED[args.workload]()
         draws = args.draws or 8192
         shard_world, shard_rank = 1, 0  # replicas: every rank runs complete evaluations
+        if args.shard_of > 1:  # also report site sharding of a small alignment (projection)
+            if world > 1:
+                raise SystemExit("bench.py: --shard-of is a one-GPU projection; run it without a launcher")
+            shard_world = args.shard_of
     else:
         prob = synthetic_problem(args.sites)
         draws = args.draws or 1
@@ -561,7 +565,7 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": 1e3 * elapsed / args.steps,
             "higher_is_better": True,
-            "scaling": "weak" if batched else "strong",
+            "scaling": "weak" if batched and args.shard_of <= 1 else "strong",
             "vs_baseline": None,
             "dtype": "f64",
             "data": DATA[args.workload],
