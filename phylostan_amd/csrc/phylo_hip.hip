@@ -1784,7 +1784,7 @@ struct phy_ctx {
   // small host-buffer evaluations (phy_eval with n <= PIN_DRAWS): inputs packed
   // into one pinned staging buffer and one device buffer (one H2D copy), the
   // output rows back through pinned memory (asynchronous DMA both ways); the
-  // draws' eigensystems are formed on the host (stage_small) and ride along
+  // eigensystems of up to 32 draws are formed on the host (stage_small) and ride along
   double* h_in = nullptr;   // pinned [PIN_DRAWS][B + model_len + EIG_LEN]
   double* h_out = nullptr;  // pinned [PIN_DRAWS][full output row]
   double* d_in = nullptr;   // device [PIN_DRAWS][B + model_len + EIG_LEN]
@@ -2571,12 +2571,20 @@ int alloc_wg_buffers(phy_ctx* c, long cap) {
 // order as eig_kernel and the C oracle, with no FMA contraction, so the same
 // bits; formed on the device by one lane per pmat wave they took 13 us of a
 // 4-draw fluA call -- a serial chain of divisions and square roots) packed
-// for one H2D copy.  Returns the doubles to copy.
-size_t stage_small(phy_ctx* ctx, int n, const double* blens, const double* model) {
+// for one H2D copy.  Up to EIG_HOST_MAX draws (the host takes ~0.6 us per
+// draw; measured per call: fluA 32 draws 175 us host-formed against 186-199
+// device-formed, 100 draws 207-210 device-formed against 237-242): beyond
+// that eig_kernel forms them, one thread per draw.
+// Returns the doubles to copy; *host_eig says whether they include the
+// eigensystems.
+constexpr int EIG_HOST_MAX = 32;
+size_t stage_small(phy_ctx* ctx, int n, const double* blens, const double* model, bool* host_eig) {
   const int ml = 10 + 2 * ctx->C;
   const size_t nb = (size_t)n * ctx->B, nm = (size_t)n * ml;
   std::memcpy(ctx->h_in, blens, sizeof(double) * nb);
   std::memcpy(ctx->h_in + nb, model, sizeof(double) * nm);
+  *host_eig = n <= EIG_HOST_MAX;
+  if (!*host_eig) return nb + nm;
   double* eg = ctx->h_in + nb + nm;
   for (int d = 0; d < n; ++d) eig_record(model + (size_t)d * ml, ctx->kind, eg + (size_t)d * EIG_LEN);
   return nb + nm + (size_t)n * EIG_LEN;
@@ -2943,10 +2951,12 @@ int phy_eval_submit(phy_ctx* ctx, int n_draws, const double* blens, const double
   const int ml = 10 + 2 * ctx->C;
   const size_t nb = (size_t)n_draws * ctx->B, nm = (size_t)n_draws * ml;
   const size_t no = (size_t)n_draws * phy_output_len(ctx);
-  const size_t nin = stage_small(ctx, n_draws, blens, model);
+  bool heig = false;
+  const size_t nin = stage_small(ctx, n_draws, blens, model, &heig);
   int rc = launch_graphed(ctx, n_draws, ctx->h_in, ctx->d_in, ctx->h_out, nullptr, st, [&]() -> int {
     HIP_TRY(hipMemcpyAsync(ctx->d_in, ctx->h_in, sizeof(double) * nin, hipMemcpyHostToDevice, st));
-    int r = launch(ctx, n_draws, ctx->d_in, ctx->d_in + nb, ctx->d_out, nullptr, st, ctx->d_in + nb + nm);
+    int r = launch(ctx, n_draws, ctx->d_in, ctx->d_in + nb, ctx->d_out, nullptr, st,
+                   heig ? ctx->d_in + nb + nm : nullptr);
     if (r) return r;
     HIP_TRY(hipMemcpyAsync(ctx->h_out, ctx->d_out, sizeof(double) * no, hipMemcpyDeviceToHost, st));
     return PHY_OK;
@@ -2988,11 +2998,13 @@ int phy_eval(phy_ctx* ctx, int n_draws, const double* blens, const double* model
   if (n_draws <= PIN_DRAWS && ctx->h_in && ctx->h_out && ctx->d_in) {  // the small-batch (sampler) path
     const size_t nb = (size_t)n_draws * ctx->B, nm = (size_t)n_draws * ml;
     const size_t no = (size_t)n_draws * phy_output_len(ctx);
-    const size_t nin = stage_small(ctx, n_draws, blens, model);
+    bool heig = false;
+    const size_t nin = stage_small(ctx, n_draws, blens, model, &heig);
     double* dsite = site_ll ? ctx->d_site : nullptr;
     int rc = launch_graphed(ctx, n_draws, ctx->h_in, ctx->d_in, ctx->h_out, dsite, st, [&]() -> int {
       HIP_TRY(hipMemcpyAsync(ctx->d_in, ctx->h_in, sizeof(double) * nin, hipMemcpyHostToDevice, st));
-      int r = launch(ctx, n_draws, ctx->d_in, ctx->d_in + nb, ctx->d_out, dsite, st, ctx->d_in + nb + nm);
+      int r = launch(ctx, n_draws, ctx->d_in, ctx->d_in + nb, ctx->d_out, dsite, st,
+                     heig ? ctx->d_in + nb + nm : nullptr);
       if (r) return r;
       HIP_TRY(hipMemcpyAsync(ctx->h_out, ctx->d_out, sizeof(double) * no, hipMemcpyDeviceToHost, st));
       return PHY_OK;
