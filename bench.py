@@ -469,16 +469,24 @@ def main():
         bl4, mv4 = blens[0][:4].copy(), mvs[0][:4].copy()
         bl100 = np.concatenate([blens[0]] * (1 + 100 // draws))[:100].copy()
         mv100 = np.concatenate([mvs[0]] * (1 + 100 // draws))[:100].copy()
-        for name in ("pattern", "resident"):
+        def sampler_ctx(name, n):
+            # sized as the CLI sizes its contexts: max_draws = the draws of one call
+            # (a 4-chain NUTS context plans for 4 draws, an ELBO context for 100)
             lk = TreeLikelihood(prob["tipcodes"], prob["weights"], prob["peel0"], prob["rooted"], prob["model"],
-                                C, max_draws=100, device=local)
+                                C, max_draws=n, device=local)
             lk.set_output(compact=True)
             try:
                 lk.set_engine(name)
             except Exception:  # the resident sweep refuses trees that do not fit (e.g. unrooted DS1)
+                lk.close()
+                return None
+            return lk
+
+        for name in ("pattern", "resident"):
+            lk = sampler_ctx(name, 4)
+            if lk is None:
                 sampler[name + "_us_per_call"] = None
                 draws_100[name] = None
-                lk.close()
                 continue
             for _ in range(20):
                 lk.evaluate_rows(bl4, mv4)
@@ -486,6 +494,8 @@ def main():
             for _ in range(300):
                 lk.evaluate_rows(bl4, mv4)
             sampler[name + "_us_per_call"] = 1e6 * (time.perf_counter() - ta) / 300
+            lk.close()
+            lk = sampler_ctx(name, 100)
             for _ in range(5):
                 lk.evaluate_rows(bl100, mv100)
             ta = time.perf_counter()
