@@ -104,13 +104,30 @@ constexpr int RD_MAX = PHY_RD_MAX;  // deepest rebuild chain: a cherry plus up t
 // 16-bit fields are signed (-1 = none).  One s_load_dwordx8 per step, issued
 // a step ahead, replaces a chain of dependent scalar loads.
 constexpr int PSTEP = 8;
+// The two-column kernel (K = 2, the batched throughput plan) reads the
+// host's 16-int steps as they are (one s_load_dwordx16, no field
+// extraction): measured 6.07-6.09 against 6.14 ms per fluA launch; the
+// one-column latency kernel keeps the packed form (64-draw calls 181
+// against 191 us with unpacked records).
+constexpr int USTEP = STEP_INTS;
 struct Step {
   int x, y, mx, my, mv, vs, fl, xs, ys, xd, vd, ch, m0, mn, rd;
 };
 __device__ __forceinline__ int lo16(int w) { return (int)(short)(w & 0xFFFF); }
 __device__ __forceinline__ int hi16(int w) { return w >> 16; }
 __device__ __forceinline__ int b8(int w, int k) { return (int)(signed char)((w >> (8 * k)) & 0xFF); }
+template <bool UNP>
 __device__ __forceinline__ Step ld_step(const int* __restrict__ prog, int s) {
+  if constexpr (UNP) {
+    const int4* q = reinterpret_cast<const int4*>(prog + s * USTEP);
+    const int4 a = q[0], b = q[1], c = q[2], d = q[3];
+    Step t;
+    t.x = a.x; t.y = a.y; t.mx = a.z; t.my = a.w;   // ST_X .. ST_MY
+    t.mv = b.x; t.vs = b.y; t.fl = b.z; t.xs = b.w;  // ST_MV .. ST_XSLOT
+    t.ys = c.x; t.xd = c.y; t.vd = c.z; t.ch = c.w;  // ST_YSLOT .. ST_CHUNK
+    t.m0 = d.x; t.mn = d.y; t.rd = d.w;              // ST_M0, ST_MN, (ST_NODE), ST_RD
+    return t;
+  }
   const int4 a = *reinterpret_cast<const int4*>(prog + s * PSTEP);
   const int4 b = *reinterpret_cast<const int4*>(prog + s * PSTEP + 4);
   Step t;
@@ -860,7 +877,7 @@ __global__ void __launch_bounds__(MAXT) __attribute__((amdgpu_waves_per_eu(MAXT 
     #define FSTEP(s, dcur, dnext, st, sn) do {                                            \
       {                                                                                   \
         const bool more = s + 1 < nsteps;                                                 \
-        sn = ld_step(prog, more ? s + 1 : s); /* next step's record, a step ahead */      \
+        sn = ld_step<K == 2>(prog, more ? s + 1 : s); /* next step's record, a step ahead */      \
         /* an x operand whose deep entry is global is read back from x's scratch slot */  \
         const bool need = more && (sn.fl & F_XDEEP) && sn.xd >= ndl;                      \
         if (!DL)                                                                                                      \
@@ -925,7 +942,7 @@ __global__ void __launch_bounds__(MAXT) __attribute__((amdgpu_waves_per_eu(MAXT 
       V4 dA[K], dB[K];
 #pragma unroll
       for (int k = 0; k < K; ++k) dA[k] = {0.0, 0.0, 0.0, 0.0};  // step 0 has no internal child
-      Step sA = ld_step(prog, 0), sB;
+      Step sA = ld_step<K == 2>(prog, 0), sB;
       for (int s = 0;;) {
         FSTEP(s, dA, dB, sA, sB);
         if (++s >= nsteps) break;
@@ -984,7 +1001,7 @@ __global__ void __launch_bounds__(MAXT) __attribute__((amdgpu_waves_per_eu(MAXT 
     };
     #define LOAD_SET(s, r) do {                                                  \
       const bool ok = s >= 0;                                                    \
-      r.st = ld_step(prog, ok ? s : 0);                                   \
+      r.st = ld_step<K == 2>(prog, ok ? s : 0);                                   \
       const int x = r.st.x, y = r.st.y, fl = r.st.fl;                     \
       /* a rebuilt cherry (F_PREVREC) is the previous-step child: y when y is       \
          internal, else x -- its operand is not loaded */                           \
@@ -1026,11 +1043,11 @@ __global__ void __launch_bounds__(MAXT) __attribute__((amdgpu_waves_per_eu(MAXT 
       if (d == 1) {                                                                       \
         REBUILD(vst, out);                                                                \
       } else {                                                                            \
-        const Step cb_ = ld_step(prog, s - d);                                            \
+        const Step cb_ = ld_step<K == 2>(prog, s - d);                                            \
         V4 acc_[K];                                                                       \
         REBUILD(cb_, acc_);                                                               \
         for (int j_ = d - 1; j_ >= 2; --j_) {                                             \
-          const Step v_ = ld_step(prog, s - j_);                                          \
+          const Step v_ = ld_step<K == 2>(prog, s - j_);                                          \
           CHAIN_UP(v_, acc_, acc_);                                                       \
         }                                                                                 \
         CHAIN_UP(vst, acc_, out);                                                         \
@@ -1849,7 +1866,8 @@ void free_ctx(phy_ctx* c) {
 // while y's subtree runs.  Those waits nest, so they live on a stack whose
 // entry per wait is fixed here (ST_XDPOS / ST_VDPOS), used by both passes.
 // Device layout of the program (see Step / ld_step): 8 packed ints per step.
-std::vector<int> pack_program(const std::vector<int>& prog) {
+std::vector<int> pack_program(const std::vector<int>& prog, bool unpacked = false) {
+  if (unpacked) return prog;  // the K = 2 kernel's form
   const size_t n = prog.size() / STEP_INTS;
   std::vector<int> out(n * PSTEP, 0);
   auto h = [](int lo, int hi) { return (int)(((unsigned)(lo & 0xFFFF)) | ((unsigned)hi << 16)); };
@@ -2183,7 +2201,7 @@ int plan_chunks(phy_ctx* c) {
     }
   }
   {
-    const std::vector<int> packed = pack_program(c->prog);
+    const std::vector<int> packed = pack_program(c->prog, K == 2);
     HIP_TRY(hipMemcpy(c->d_prog, packed.data(), packed.size() * sizeof(int), hipMemcpyHostToDevice));
   }
   c->cap_m = cap;
