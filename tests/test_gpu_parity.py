@@ -421,3 +421,19 @@ def test_tuning_grows_workgroup_regions_past_create():
     _close(got.dLdP, ref.dLdP, RTOL_G, "dLdP")
     check_case(case, eng, got)
 
+
+
+@pytest.mark.parametrize("engine", ["pattern", "class", "resident"])
+@pytest.mark.parametrize("S,rooted,max_draws", [(3, True, 1), (3, False, 1), (4, False, 1), (3, True, 4096),
+                                                (3, False, 4096)],
+                         ids=["S3-rooted", "S3-unrooted", "S4-unrooted", "S3-rooted-batched", "S3-unrooted-batched"])
+def test_minimal_trees(engine, S, rooted, max_draws):
+    """The smallest trees the boundary accepts (S = 3; an unrooted tree's root
+    then has a tip child on the merged branch), on every engine, with the
+    sampler's one-column plan (max_draws 1) and the batched two-column plan."""
+    if engine == "resident" and not rooted:
+        pytest.skip("the resident sweep takes rooted trees only (test_resident_refuses_unrooted)")
+    case = cases.random_case(31 + S, S=S, P=7, C=2, model="GTR", rooted=rooted)
+    eng = _engine(case, max_draws=max_draws)
+    eng.set_engine(engine)
+    check_case(case, eng)
