@@ -437,3 +437,20 @@ def test_minimal_trees(engine, S, rooted, max_draws):
     eng = _engine(case, max_draws=max_draws)
     eng.set_engine(engine)
     check_case(case, eng)
+
+
+@pytest.mark.parametrize("engine", ["pattern", "class", "resident"])
+def test_zero_and_saturated_branches_and_zero_weights(engine):
+    """Internal branch lengths of zero (P = I, dP/dt = Q; a zero tip branch
+    would make patterns impossible) and branches of 40 substitutions (P at
+    the stationary distribution, vanishing gradients), and patterns of weight
+    zero (present in the alignment, no contribution)."""
+    case = cases.random_case(41, S=16, P=90, C=3, model="GTR")
+    case.blens[case.S::3] = 0.0  # branch b sits above node b + 1: b >= S are internal
+    case.blens[1::5] = 40.0
+    case.weights[::7] = 0.0
+    ref = case.oracle()
+    assert np.isfinite(ref["loglik"])
+    eng = _engine(case)
+    eng.set_engine(engine)
+    check_case(case, eng)
