@@ -454,3 +454,24 @@ def test_zero_and_saturated_branches_and_zero_weights(engine):
     eng = _engine(case)
     eng.set_engine(engine)
     check_case(case, eng)
+
+
+@pytest.mark.parametrize("engine", ["pattern", "class", "resident"])
+@pytest.mark.parametrize("max_draws", [8, 4096], ids=["one-column", "batched"])
+def test_impossible_draw_inside_a_batch(engine, max_draws):
+    """One draw of a batch with L = 0 (mixture weights all zero) comes back
+    as -inf; its neighbours' rows equal their single-draw rows bit for bit
+    (nothing of the impossible draw leaks through shared slots or sums)."""
+    case = cases.random_case(51, S=12, P=80, C=2, model="HKY")
+    eng = _engine(case, max_draws=max_draws)
+    eng.set_engine(engine)
+    n = 5
+    bl = np.repeat(case.blens[None], n, axis=0) * np.linspace(0.8, 1.2, n)[:, None]
+    mv = np.repeat(case.model_vec()[None], n, axis=0)
+    mv[2, 10 + case.C:] = 0.0
+    rows = eng.evaluate_rows(bl, mv)
+    assert rows[2, 0] == -np.inf
+    for k in (0, 1, 3, 4):
+        one = eng.evaluate_rows(bl[k:k + 1], mv[k:k + 1])[0]
+        assert np.array_equal(rows[k], one), k
+        assert np.isfinite(rows[k]).all()
