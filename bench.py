@@ -64,6 +64,11 @@ def parse():
                     help="evaluate only the first of this many pattern shards on one GPU, with no collective -- "
                          "what each rank of a site-sharded N-GPU run computes (a projection, not the headline; "
                          "for the batched workloads, SURVEY 8e's site sharding beside the replicas)")
+    ap.add_argument("--multi-device", type=int, default=0,
+                    help="one process, ONE context over this many devices (phy_create_multi: pattern shards on "
+                         "devices 0..N-1, one RCCL all-reduce of the output rows inside the C-ABI, or a device-side "
+                         "sum when the box has fewer GPUs than shards -- the reference boundary's single handle, "
+                         "eigen/prune_stan.hpp:9-17); parallelism multidevN")
     ap.add_argument("--dry-run", action="store_true",
                     help="launcher check only: ranks join a gloo group on the CPU, all-reduce their rank "
                          "ids and exit (no GPU, no evaluation)")
@@ -310,6 +315,24 @@ def main():
 
     from phylostan_amd.distributed import ShardedLikelihood
 
+    class MultiDeviceLikelihood:
+        """bench's view of one phy_create_multi context (--multi-device N):
+        shards on devices 0..N-1 (all on device 0 when the box has fewer GPUs:
+        the device-side shard sum), inputs and rows on device 0."""
+
+        def __init__(self, prob, C, n, max_draws):
+            from phylostan_amd.engine import TreeLikelihood
+            ndev = torch.cuda.device_count()
+            self.devices = list(range(n)) if ndev >= n else [0] * n
+            self.engine = TreeLikelihood(prob["tipcodes"], prob["weights"], prob["peel0"], prob["rooted"],
+                                         prob["model"], C, max_draws=max_draws, devices=self.devices)
+            self.p0, self.p1 = 0, prob["tipcodes"].shape[1]
+            self.world = 1
+
+        def evaluate(self, d_blens, d_model, d_out, stream=None):
+            self.engine.evaluate_device(d_blens.data_ptr(), d_model.data_ptr(), d_out.data_ptr(), 0,
+                                        n_draws=d_blens.shape[0], stream=stream or 0)
+
     batched = args.workload in BATCHED
     if batched:
         prob = BATCHED[args.workload]()
@@ -330,8 +353,14 @@ def main():
     S, P = prob["tipcodes"].shape
     C = prob["C"]
 
-    sl = ShardedLikelihood(prob["tipcodes"], prob["weights"], prob["peel0"], prob["rooted"], prob["model"],
-                           C, shard_rank, shard_world, device=local, max_draws=draws)
+    if args.multi_device:
+        if world > 1 or args.shard_of > 1:
+            raise SystemExit("bench.py: --multi-device is one process driving N devices; run it without a launcher "
+                             "and without --shard-of")
+        sl = MultiDeviceLikelihood(prob, C, args.multi_device, draws)
+    else:
+        sl = ShardedLikelihood(prob["tipcodes"], prob["weights"], prob["peel0"], prob["rooted"], prob["model"],
+                               C, shard_rank, shard_world, device=local, max_draws=draws)
     if args.shard_of > 1:
         sl.world = 1  # the projection: one shard's evaluation, no collective
     eng = sl.engine
@@ -570,12 +599,12 @@ def main():
             "metric": METRIC[args.workload],
             "value": value,
             "unit": "evals/s",
-            "n_gpus": world,
+            "n_gpus": len(set(sl.devices)) if args.multi_device else world,
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": 1e3 * elapsed / args.steps,
             "higher_is_better": True,
-            "scaling": "weak" if batched and args.shard_of <= 1 else "strong",
+            "scaling": "weak" if batched and args.shard_of <= 1 and not args.multi_device else "strong",
             "vs_baseline": None,
             "dtype": "f64",
             "data": DATA[args.workload],
@@ -586,7 +615,9 @@ def main():
                     args.workload, "synthetic 128 x %d sites GTR+W4, pattern-sharded" % args.sites),
                 "taxa": S, "patterns": P, "patterns_per_rank": P_local, "categories": C,
                 "branches": B, "draws_per_step": draws,
-                "parallelism": ("replicas%d" % world) if batched else ("patterns%d" % world),
+                "parallelism": ("multidev%d" % args.multi_device) if args.multi_device else
+                               ("replicas%d" % world) if batched else ("patterns%d" % world),
+                "devices": sl.devices if args.multi_device else None,
                 "projection_shard_of": args.shard_of or None,
             },
             "roofline": {

@@ -67,9 +67,50 @@ class PhyloHipError(RuntimeError):
     pass
 
 
+class _TorchAfterEngineGuard:
+    """Import hook installed when the library is loaded in a process that has
+    not imported torch.  The PyTorch wheel bundles its own HIP runtime; once
+    this library's runtime (ROCm's) holds the GPU, a torch imported later
+    fails its GPU initialisation with a misleading "No HIP GPUs are
+    available" (INTEGRATION.md, "PyTorch in the same process";
+    tools/dbg_torch_after.py).  The guard turns that into a clear error at
+    the ``import torch`` that causes it."""
+
+    def find_spec(self, name, path=None, target=None):
+        if name == "torch" and _lib is not None:
+            raise ImportError(
+                "phylostan_amd: torch imported after libphylo_hip.so was loaded; torch's bundled HIP runtime "
+                "cannot initialise the GPU after the engine's runtime holds it.  Import torch before "
+                "phylostan_amd's engine (or set PHYLO_NO_TORCH=1 before loading to disable this guard in a "
+                "process that must not import torch at all).")
+        return None
+
+
+def _order_runtimes():
+    """Make the two HIP runtimes' order correct by construction: import torch
+    (loaded, not initialised: ~1.5 s, no GPU work) before the engine's
+    library when torch is installed; where it is not installed, or
+    PHYLO_NO_TORCH=1 says the process must not import it, install the guard
+    so a later ``import torch`` fails loudly instead of leaving torch without
+    a GPU."""
+    import importlib.util
+    import sys
+    if "torch" in sys.modules:
+        return
+    if os.environ.get("PHYLO_NO_TORCH") != "1" and importlib.util.find_spec("torch") is not None:
+        import torch  # noqa: F401
+        return
+    if not any(isinstance(f, _TorchAfterEngineGuard) for f in sys.meta_path):
+        sys.meta_path.insert(0, _TorchAfterEngineGuard())
+
+
 def load(path=None):
     """Load (once) and return the library.  Raises ``PhyloHipError`` if the
-    HIP library has not been built -- the product has no CPU fallback."""
+    HIP library has not been built or does not export every entry point of
+    ``include/phylo_hip.h`` -- the product has no CPU fallback and no partial
+    binding.  ``PHYLO_HIP_AB=1`` (same-box A/B runs of older variant builds,
+    ``PHYLO_HIP_LIB``) binds what the variant exports and prints the missing
+    names once."""
     global _lib
     if _lib is not None and path is None:
         return _lib
@@ -78,16 +119,22 @@ def load(path=None):
         raise PhyloHipError(
             "HIP library %s is missing: build it with `python -c 'import __graft_entry__ as g; g.build()'` "
             "(there is no CPU fallback in phylostan_amd)" % p)
+    _order_runtimes()
     lib = ctypes.CDLL(p)
+    missing = []
     for name, (res, args) in SIGNATURES.items():
         try:
             fn = getattr(lib, name)
         except AttributeError:
-            if os.environ.get("PHYLO_HIP_LIB"):  # an older variant build under A/B measurement
-                continue
-            raise PhyloHipError("%s does not export %s (stale build?)" % (p, name))
+            missing.append(name)
+            continue
         fn.restype = res
         fn.argtypes = args
+    if missing:
+        if os.environ.get("PHYLO_HIP_AB") != "1":
+            raise PhyloHipError("%s does not export %s (stale build?)" % (p, ", ".join(missing)))
+        import sys
+        print("phylostan_amd: A/B variant %s lacks %s" % (p, ", ".join(missing)), file=sys.stderr)
     if path is None:
         _lib = lib
     return lib

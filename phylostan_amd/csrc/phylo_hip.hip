@@ -52,13 +52,6 @@
 namespace {
 
 constexpr int WAVE = 64;
-#ifndef PHY_ABLATE
-// Diagnostic builds only (timing of the sweep's pieces; results are wrong by
-// construction): 2 = no reverse pass, 4 = no per-draw epilogue, 8 = no
-// moved-partial stores, 16 = every store to entry 0 (L2-resident), 32 =
-// every operand load from entry 0.
-#define PHY_ABLATE 0
-#endif
 // Program step (STEP_INTS ints, host-built by build_program).
 constexpr int STEP_INTS = 16;
 enum {
@@ -728,7 +721,7 @@ __global__ void __launch_bounds__(MAXT) __attribute__((amdgpu_waves_per_eu(MAXT 
 #pragma unroll
   for (int k = 0; k < K; ++k) lcol[k] = (uint32_t)((k * 2 * ncolwg + colw) * 16);
   auto ent = [&](bool use, int e) __attribute__((always_inline)) -> uint32_t {  // uniform part
-    return use ? ((PHY_ABLATE & 32) ? 0u : (uint32_t)e * estr) : OOB;
+    return use ? (uint32_t)e * estr : OOB;
   };
   // Scratch offsets of this lane's live columns only: padding columns
   // (pattern >= P) get the column part OOB, so they neither store nor load
@@ -737,7 +730,7 @@ __global__ void __launch_bounds__(MAXT) __attribute__((amdgpu_waves_per_eu(MAXT 
   // exactly zero.
   uint32_t lofs[K];  // per block: lcol[k], or OOB on a padding column
   auto soff = [&](int e, int k) __attribute__((always_inline)) -> uint32_t {
-    return lofs[k] + ((PHY_ABLATE & 16) ? 0u : (uint32_t)e * estr);
+    return lofs[k] + (uint32_t)e * estr;
   };
   auto put = [&](double2* base, int e, int k, const V4& v) __attribute__((always_inline)) {
     double2* d = base + ((size_t)e * K + k) * 2 * ncolwg + colw;
@@ -925,7 +918,7 @@ __global__ void __launch_bounds__(MAXT) __attribute__((amdgpu_waves_per_eu(MAXT 
           for (int k = 0; k < K; ++k) av[k] = pv[k];                                                                  \
         }                                                                                                             \
       _Pragma("unroll")                                                                                               \
-        for (int k = 0; k < K; ++k) if (!(PHY_ABLATE & 8) && !(fl & F_NOSTORE)) st_v4(srd_scr, soff(vs, k), half_bytes, av[k]);                                    \
+        for (int k = 0; k < K; ++k) if (!(fl & F_NOSTORE)) st_v4(srd_scr, soff(vs, k), half_bytes, av[k]);                                    \
         if (fl & F_VDEEP) {                                                                                           \
           const int dp = st.vd;                                                                                \
           if (DL || dp < ndl)  /* a global entry is x's scratch slot itself */                                        \
@@ -1151,7 +1144,7 @@ __global__ void __launch_bounds__(MAXT) __attribute__((amdgpu_waves_per_eu(MAXT 
       else if (yt_) RSTEP_V(s, cs, cn, false, true);     \
       else RSTEP_V(s, cs, cn, false, false);             \
     } while (0)
-    if (!(PHY_ABLATE & 2)) {
+    {
       int s = nsteps - 1;
       CSet A, Bs;
       LOAD_SET(s, A);
@@ -1184,7 +1177,7 @@ __global__ void __launch_bounds__(MAXT) __attribute__((amdgpu_waves_per_eu(MAXT 
     ss[4] = acc_f.z;
     ss[5] = acc_f.w;
   }
-  if (a.g_direct && !(PHY_ABLATE & 4)) {
+  if (a.g_direct) {
     // One workgroup per draw: this wave's slot is the draw's dL/dP for
     // category c.  Write the output rows (branch order) and the chain-rule
     // inner products <G_cb, Q P_cb> (dP/dt = Q P), 16 lanes per matrix.
@@ -1446,13 +1439,17 @@ __global__ void __launch_bounds__(64) eig_kernel(PmatArgs a) {
 // record per lane straight to HBM would scatter every store instruction).
 constexpr int PMAT_WAVE_RECS = 64;
 constexpr int EIG_FUSE_MAX = 32;  // draws per launch up to which pmat_kernel forms the eigensystems
+// WITH_EIG is a template parameter, not a runtime flag: the inlined Jacobi's
+// registers would otherwise be allocated in the batched kernel too (round 3:
+// 0.158 -> 0.249 ms per fluA launch of 8192 draws when it was a runtime flag).
+template <bool WITH_EIG>
 __global__ void __launch_bounds__(64) pmat_kernel(PmatArgs a) {
   __shared__ double e[EIG_LEN];
   extern __shared__ __attribute__((aligned(16))) double recl[];  // [64][R*4]
   const int draw = blockIdx.y;
   const int C = a.C, nmat = a.nmat;
   const int lane = threadIdx.x;
-  if (a.with_eig) {  // a serial chain of one thread: every wave of the draw forms it (no eig launch)
+  if constexpr (WITH_EIG) {  // a serial chain of one thread: every wave of the draw forms it (no eig launch)
     if (lane == 0) {
       eig_record(a.model + (size_t)draw * (10 + 2 * C), a.kind, e);
       if (blockIdx.x == 0)
@@ -2275,13 +2272,13 @@ int timing_begin(phy_ctx* ctx, hipStream_t st, hipEvent_t* e0, hipEvent_t* e1) {
   return PHY_OK;
 }
 
-void launch_finalize(const FinArgs& fa, int n, hipStream_t st);
+bool launch_finalize(FinArgs fa, int n, hipStream_t st);
 
 // The class sweep (class_engine.inc): forward levels, root, reverse levels,
 // then the ordered dL/dP sums and the shared finalize.  The timed region
 // (phy_timing_*) spans the forward through the last reverse level.
 int launch_class(phy_ctx* ctx, int n, const double* d_blens, const double* d_model, double* d_out,
-                 double* d_site, hipStream_t st, double* grows, long long gstride) {
+                 double* d_site, hipStream_t st, double* grows, long long gstride, bool* qdone) {
   ClassEngine* e = ctx->ce;
   const int C = ctx->C, B = ctx->B;
   if ((long)n * C > 65535) return fail(PHY_ERANGE, "class sweep: n_draws * C must be <= 65535");
@@ -2346,7 +2343,7 @@ int launch_class(phy_ctx* ctx, int n, const double* d_blens, const double* d_mod
   FinArgs fa{ctx->d_gslot, e->d_sslot, ctx->d_pmat, ctx->eig_cur, d_blens, d_model, ctx->d_gpos, ctx->d_inner, d_out,
              C,            B,          ctx->nmat,   e->nrootch,  phy_output_len(ctx), 0, ctx->R, grows, gstride,
              ctx->kind,    0,          ctx->qfuse_pref ? 1 : 0};
-  launch_finalize(fa, n, st);
+  *qdone = launch_finalize(fa, n, st);
   HIP_TRY(hipGetLastError());
   return PHY_OK;
 }
@@ -2354,10 +2351,18 @@ int launch_class(phy_ctx* ctx, int n, const double* d_blens, const double* d_mod
 int launch_pattern(phy_ctx* ctx, int n, const double* d_blens, const double* d_model, double* d_out,
                    double* d_site, hipStream_t st, double* grows, long long gstride, bool* qdone = nullptr);
 
-void launch_finalize(const FinArgs& fa, int n, hipStream_t st) {
+// Returns whether the finalize ran the Q-parameter chain rule too: when its
+// LDS ([C][B] inner products, Q, the reduction rows and the chain rule's
+// QG_SHARED) would pass the 160 KiB cap the chain rule is left to
+// qgrad_kernel (large C*B; finalize_kernel is opted into LDS_CAP at
+// phy_create, and phy_create refuses a C*B whose finalize alone cannot fit).
+bool launch_finalize(FinArgs fa, int n, hipStream_t st) {
   const int threads = 1024;
-  hipLaunchKernelGGL(finalize_kernel, dim3(n), dim3(threads),
-                     ((size_t)fa.C * fa.B + 16 + threads + (fa.qf ? QG_SHARED : 0)) * sizeof(double), st, fa);
+  const size_t base = (size_t)fa.C * fa.B + 16 + threads;
+  if (fa.qf && (base + QG_SHARED) * sizeof(double) > LDS_CAP) fa.qf = 0;
+  hipLaunchKernelGGL(finalize_kernel, dim3(n), dim3(threads), (base + (fa.qf ? QG_SHARED : 0)) * sizeof(double), st,
+                     fa);
+  return fa.qf != 0;
 }
 
 // The resident class sweep (resident_engine.inc): forward + root L, then the
@@ -2365,7 +2370,7 @@ void launch_finalize(const FinArgs& fa, int n, hipStream_t st) {
 // (the reverse writes the dL/dP rows itself); the shared finalize.  The
 // timed region spans the two sweep kernels.
 int launch_res(phy_ctx* ctx, int n, const double* d_blens, const double* d_model, double* d_out,
-               double* d_site, hipStream_t st, double* grows, long long gstride) {
+               double* d_site, hipStream_t st, double* grows, long long gstride, bool* qdone) {
   ResEngine* e = ctx->re;
   const int C = ctx->C, B = ctx->B;
   int rc = res_engine_reserve(e, n);
@@ -2384,7 +2389,7 @@ int launch_res(phy_ctx* ctx, int n, const double* d_blens, const double* d_model
   FinArgs fa{ctx->d_gslot, e->d_sslot, ctx->d_pmat, ctx->eig_cur, d_blens, d_model, ctx->d_gpos, ctx->d_inner, d_out,
              C,            B,          ctx->nmat,   1,           phy_output_len(ctx), 0, ctx->R, grows, gstride,
              ctx->kind,    0,          ctx->qfuse_pref ? 1 : 0};
-  launch_finalize(fa, n, st);
+  *qdone = launch_finalize(fa, n, st);
   HIP_TRY(hipGetLastError());
   return PHY_OK;
 }
@@ -2404,17 +2409,21 @@ int launch(phy_ctx* ctx, int n, const double* d_blens, const double* d_model, do
       hipLaunchKernelGGL(eig_kernel, dim3((n + 63) / 64), dim3(64), 0, st, pa);
       HIP_TRY(hipGetLastError());
     }
-    hipLaunchKernelGGL(pmat_kernel, dim3((C * ctx->nmat + PMAT_WAVE_RECS - 1) / PMAT_WAVE_RECS, n), dim3(64),
-                       (size_t)PMAT_WAVE_RECS * ctx->R * 4 * sizeof(double), st, pa);
+    const dim3 pgrid((C * ctx->nmat + PMAT_WAVE_RECS - 1) / PMAT_WAVE_RECS, n);
+    const size_t plds = (size_t)PMAT_WAVE_RECS * ctx->R * 4 * sizeof(double);
+    if (with_eig)
+      hipLaunchKernelGGL(pmat_kernel<true>, pgrid, dim3(64), plds, st, pa);
+    else
+      hipLaunchKernelGGL(pmat_kernel<false>, pgrid, dim3(64), plds, st, pa);
     HIP_TRY(hipGetLastError());
   }
   double* grows = ctx->compact ? ctx->d_grows : d_out + PHY_OUT_G(B, C);
   const long long gstride = ctx->compact ? (long long)16 * C * B : (long long)phy_output_len(ctx);
   // the chain rule runs inside the sweep (one workgroup per draw) or the
   // finalize kernel unless PHY_QFUSE=0
-  bool qdone = ctx->qfuse_pref && ctx->engine != 0;
-  int rc0 = ctx->engine == 1   ? launch_class(ctx, n, d_blens, d_model, d_out, d_site, st, grows, gstride)
-            : ctx->engine == 2 ? launch_res(ctx, n, d_blens, d_model, d_out, d_site, st, grows, gstride)
+  bool qdone = false;
+  int rc0 = ctx->engine == 1   ? launch_class(ctx, n, d_blens, d_model, d_out, d_site, st, grows, gstride, &qdone)
+            : ctx->engine == 2 ? launch_res(ctx, n, d_blens, d_model, d_out, d_site, st, grows, gstride, &qdone)
                                : launch_pattern(ctx, n, d_blens, d_model, d_out, d_site, st, grows, gstride, &qdone);
   if (rc0) return rc0;
   if (!qdone) {
@@ -2546,11 +2555,12 @@ int launch_pattern(phy_ctx* ctx, int n, const double* d_blens, const double* d_m
     hipLaunchKernelGGL(gsum_kernel, dim3((C * B * 16 + 63) / 64, n), dim3(256), 0, st, fa);
     HIP_TRY(hipGetLastError());
   }
+  bool fq = false;
   if (!fin) {
-    launch_finalize(fa, n, st);
+    fq = launch_finalize(fa, n, st);
     HIP_TRY(hipGetLastError());
   }
-  if (qdone) *qdone = qf != 0 || fa.qf != 0;
+  if (qdone) *qdone = qf != 0 || fq;
   return PHY_OK;
 }
 
@@ -2717,6 +2727,11 @@ int phy_create(int S, int P, int C, int rooted, int model, const uint8_t* tipcod
                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)LDS_CAP);
     (void)hipFuncSetAttribute((const void*)res_fwd_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)LDS_CAP);
     (void)hipFuncSetAttribute((const void*)res_rev_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)LDS_CAP);
+    (void)hipFuncSetAttribute((const void*)finalize_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)LDS_CAP);
+  }
+  if (((size_t)C * c->B + 16 + 1024) * sizeof(double) > LDS_CAP) {
+    delete c;
+    return fail(PHY_EINVAL, "too many branches x categories for the finalize's LDS (C * B must be <= 19,440)");
   }
   if (lds_bytes(S, C, c->R, 3, 1, 0) > LDS_CAP) {
     delete c;
@@ -2953,7 +2968,8 @@ int phy_eval_submit(phy_ctx* ctx, int n_draws, const double* blens, const double
   if (!ctx) return fail(PHY_EINVAL, "NULL ctx");
   if (ctx->ms) {
     if (ctx->ms->pending) return fail(PHY_EINVAL, "phy_eval_submit: an evaluation is already in flight");
-    if (n_draws < 1 || n_draws > ctx->max_draws) return fail(PHY_ERANGE, "n_draws out of range");
+    if (n_draws < 1 || n_draws > ctx->max_draws || n_draws > PIN_DRAWS)
+      return fail(PHY_ERANGE, "phy_eval_submit: n_draws must be in [1, min(max_draws, 128)]");
     if (!blens || !model) return fail(PHY_EINVAL, "NULL host buffer");
     int rc = multi_enqueue(ctx, n_draws, blens, model, false);
     if (rc) return rc;

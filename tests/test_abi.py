@@ -52,3 +52,50 @@ def test_missing_library_is_an_error(tmp_path):
     from phylostan_amd import _lib
     with pytest.raises(_lib.PhyloHipError):
         _lib.load(str(tmp_path / "nope.so"))
+
+
+def test_stale_build_is_refused(tmp_path, monkeypatch):
+    """A library lacking an entry point is refused at load, even when it is a
+    PHYLO_HIP_LIB variant; only PHYLO_HIP_AB=1 (A/B runs) binds a partial one."""
+    import subprocess
+    from phylostan_amd import _lib
+    src = tmp_path / "stale.c"
+    src.write_text("int phy_create(void) { return 0; }\n")
+    so = tmp_path / "stale.so"
+    subprocess.run(["gcc", "-shared", "-fPIC", "-o", str(so), str(src)], check=True)
+    monkeypatch.setenv("PHYLO_HIP_LIB", str(so))
+    monkeypatch.delenv("PHYLO_HIP_AB", raising=False)
+    with pytest.raises(_lib.PhyloHipError, match="stale build"):
+        _lib.load(str(so))
+    monkeypatch.setenv("PHYLO_HIP_AB", "1")
+    lib = _lib.load(str(so))
+    assert hasattr(lib, "phy_create")
+
+
+def test_torch_after_engine_is_a_clear_error():
+    """Run in a fresh interpreter: with PHYLO_NO_TORCH=1 the engine loads
+    without torch, and a later `import torch` raises the guard's ImportError
+    instead of leaving torch without a GPU; by default load() imports torch
+    first, so the order is right by construction."""
+    import subprocess
+    import sys
+    from phylostan_amd import _lib
+    if not os.path.exists(_lib.LIB_PATH):
+        pytest.skip("HIP library not built")
+    code = ("import sys; sys.path.insert(0, %r)\n"
+            "from phylostan_amd import _lib\n"
+            "_lib.load()\n"
+            "print('torch loaded before engine:', 'torch' in sys.modules)\n"
+            "try:\n"
+            "    import torch\n"
+            "    print('import ok')\n"
+            "except ImportError as e:\n"
+            "    print('guard:', 'imported after' in str(e))\n") % ROOT
+    env = dict(os.environ, PHYLO_NO_TORCH="1")
+    out = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=300)
+    assert "torch loaded before engine: False" in out.stdout, out.stdout + out.stderr
+    assert "guard: True" in out.stdout, out.stdout + out.stderr
+    env.pop("PHYLO_NO_TORCH")
+    out = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=300)
+    assert "torch loaded before engine: True" in out.stdout, out.stdout + out.stderr
+    assert "import ok" in out.stdout, out.stdout + out.stderr

@@ -180,20 +180,32 @@ def test_production_batch_fluA_every_row_vs_c_port():
                   "grads %.1e Q-params %.1e dLdP %.1e" % tuple(worst))
 
 
-def _synthetic_vs_c_port(n_sites, engine):
-    from oracle import cpu
-    from phylostan_amd import synthetic
-    from phylostan_amd.engine import EvalResult
-    pd, prm = synthetic.simulate(n_sites=n_sites)
-    case = cases.Case("synthetic", pd.tipcodes, pd.weights, pd.peel0, True, "GTR", 4, prm["blens"],
-                      prm["freqs"], prm["rates"], prm["rs"], prm["ps"])
-    eng = _engine(case)
+_SYNTH = {}
+
+
+def _synthetic_case_ref(n_sites):
+    """The synthetic workload and its C-port evaluation (OpenMP, cached per
+    size: the full-size tests share one)."""
+    if n_sites not in _SYNTH:
+        from oracle import cpu
+        from phylostan_amd import synthetic
+        from phylostan_amd.engine import EvalResult
+        pd, prm = synthetic.simulate(n_sites=n_sites)
+        case = cases.Case("synthetic", pd.tipcodes, pd.weights, pd.peel0, True, "GTR", 4, prm["blens"],
+                          prm["freqs"], prm["rates"], prm["rs"], prm["ps"])
+        nt = max(1, min(16, os.cpu_count() or 1))
+        out, sl = cpu.evaluate(case.tipcodes, case.weights, case.peel0, True, 2, case.model_vec(), case.blens, 4,
+                               site_ll=True, nthreads=nt)
+        _SYNTH.clear()
+        _SYNTH[n_sites] = (case, EvalResult(out, 2 * case.S - 2, 4, sl))
+    return _SYNTH[n_sites]
+
+
+def _synthetic_vs_c_port(n_sites, engine, devices=None):
+    case, ref = _synthetic_case_ref(n_sites)
+    eng = _engine(case, devices=devices)
     eng.set_engine(engine)
     res = eng.evaluate(case.blens, case.model_vec(), site_ll=True)
-    nt = max(1, min(16, os.cpu_count() or 1))
-    out, sl = cpu.evaluate(case.tipcodes, case.weights, case.peel0, True, 2, case.model_vec(), case.blens, 4,
-                           site_ll=True, nthreads=nt)
-    ref = EvalResult(out, eng.B, 4, sl)
     refd = {"site_ll": ref.site_ll, "loglik": ref.loglik, "dLdP": ref.dLdP, "grad_blens": ref.grad_blens,
             "grad_rs": ref.grad_rs, "grad_ps": ref.grad_ps, "grad_freq_root": ref.grad_freq_root}
     e = errors(res, refd, "GTR")
@@ -213,6 +225,18 @@ def test_synthetic_full_size_vs_c_port(engine):
         assert eng.program_info()["nblocks"] > 4000 and eng.lds_plan()["n_chunks"] > 1
     report.record("config 4 synthetic 128x1M (P=%d) [%s] vs C port: %s  Q-params %.1e"
                   % (case.P, engine, fmt(e), eq))
+
+
+def test_synthetic_full_size_8_shards_vs_c_port():
+    """BASELINE config 4's 8-way partition behind ONE handle: phy_create_multi
+    over 8 pattern shards of the full 1M-site workload (the one-GPU box maps
+    them all to device 0: each shard its own context, class plan and stream,
+    rows summed on the device in shard order; on a node with 8 GPUs the same
+    handle puts them on devices 0..7 and reduces with one ncclAllReduce)."""
+    case, eng, e, eq = _synthetic_vs_c_port(1_000_000, "auto", devices=[0] * 8)
+    assert eng.engine() == "class"
+    report.record("config 4 synthetic 128x1M in 8 pattern shards (phy_create_multi, P=%d) vs C port: %s  "
+                  "Q-params %.1e" % (case.P, fmt(e), eq))
 
 
 def test_class_sweep_synthetic_200k_vs_c_port():

@@ -99,3 +99,29 @@ def test_sharded_context_refusals():
         TreeLikelihood(case.tipcodes, case.weights, case.peel0, True, case.model, case.C, devices=[0] * 4)
     with pytest.raises(PhyloHipError):  # devices neither all distinct nor all the same
         TreeLikelihood(case.tipcodes, case.weights, case.peel0, True, case.model, case.C, devices=[0, 0, 1])
+
+
+def test_distinct_devices_rccl_branch():
+    """The RCCL branch of phy_create_multi (ncclCommInitAll, one group
+    ncclAllReduce of the rows, peer copies of device inputs): runs wherever
+    the box has two or more GPUs -- the one-GPU box skips it, so on that box
+    this branch is unverified."""
+    import torch
+    if torch.cuda.device_count() < 2:
+        pytest.skip("needs two devices (the one-GPU box has one)")
+    from phylostan_amd.engine import TreeLikelihood
+    case = cases.hcv_case()
+    one = TreeLikelihood(case.tipcodes, case.weights, case.peel0, case.rooted, case.model, case.C, max_draws=4)
+    multi = TreeLikelihood(case.tipcodes, case.weights, case.peel0, case.rooted, case.model, case.C, max_draws=4,
+                           devices=[0, 1])
+    rng = np.random.default_rng(5)
+    bl = case.blens[None, :] * rng.uniform(0.7, 1.3, (4, 1))
+    mv = np.repeat(case.model_vec()[None], 4, axis=0)
+    _rows_close(multi.evaluate_rows(bl, mv), one.evaluate_rows(bl, mv))
+    d_bl = torch.tensor(bl, device="cuda:0")
+    d_mv = torch.tensor(mv, device="cuda:0")
+    d_out = torch.zeros((4, multi.outlen), device="cuda:0", dtype=torch.float64)
+    multi.evaluate_device(d_bl.data_ptr(), d_mv.data_ptr(), d_out.data_ptr(), 0, n_draws=4,
+                          stream=torch.cuda.current_stream(0).cuda_stream)
+    torch.cuda.synchronize()
+    _rows_close(d_out.cpu().numpy(), one.evaluate_rows(bl, mv))

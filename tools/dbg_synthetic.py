@@ -1,7 +1,7 @@
 """Debug helper (test infrastructure, calls oracle/): the synthetic workload
 on the GPU vs the C port, per output array, with the location of the
 largest dL/dP error.  Run on the GPU box from the repository root:
-    python -m tests.dbg_synthetic [n_sites] [engine ...]
+    python -m tools.dbg_synthetic [n_sites] [engine ...]
 PHYLO_HIP_LIB selects a variant library."""
 import os
 import sys

@@ -1,5 +1,5 @@
 """Debug helper: does torch initialise the GPU after this library ran
-evaluations (graphs on / off)?  python -m tests.dbg_torch_after {0|1} [n_calls] [import_first]"""
+evaluations (graphs on / off)?  python -m tools.dbg_torch_after {0|1} [n_calls] [import_first]"""
 import sys
 
 import numpy as np

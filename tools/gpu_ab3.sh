@@ -10,7 +10,7 @@ for rep in 1 2; do
   timeout -k 10 200 python bench.py --no-cpu-baseline --steps 100 --warmup 10 --json-out $O/base_$rep.json > $O/base_$rep.log 2>&1 || exit $?
   for v in "$@"; do
     n=$(basename $v .so)
-    PHYLO_HIP_LIB=$PWD/$v timeout -k 10 200 python bench.py --no-cpu-baseline --steps 100 --warmup 10 --json-out $O/${n}_$rep.json > $O/${n}_$rep.log 2>&1 || exit $?
+    PHYLO_HIP_AB=1 PHYLO_HIP_LIB=$PWD/$v timeout -k 10 200 python bench.py --no-cpu-baseline --steps 100 --warmup 10 --json-out $O/${n}_$rep.json > $O/${n}_$rep.log 2>&1 || exit $?
   done
 done
 for f in $O/*.json; do python -c "import json; d=json.load(open('$f')); print('$f', round(d['value']), round(d['roofline']['kernel_avg_ms'],4))"; done

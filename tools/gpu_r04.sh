@@ -1,0 +1,58 @@
+#!/bin/bash
+# Round-4 GPU session script (run through gpurun from the repository root).
+#   tools/gpu_r04.sh TAG [tests] [bench] [shard8] [synth] [multidev] [prof] [lat]
+# Every GPU step has its own time limit and the steps are chained: the first
+# failure ends the script (set -e), nothing is retried.  Outputs under
+# gpurun_out/TAG/.
+set -eo pipefail
+TAG=${1:?tag}
+shift
+O=gpurun_out/$TAG
+mkdir -p $O
+export TMPDIR=/tmp
+want() { [ $# -eq 0 ] && return 0; for w in "${STEPS[@]}"; do [ "$w" = "$1" ] && return 0; done; return 1; }
+STEPS=("$@")
+[ ${#STEPS[@]} -eq 0 ] && STEPS=(tests bench shard8 synth multidev)
+
+if want tests; then
+  timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 240 --timeout-method thread \
+    > $O/pytest.log 2>&1 || { tail -30 $O/pytest.log; exit 1; }
+  tail -40 $O/pytest.log
+fi
+if want smoke; then
+  timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1
+  tail -3 $O/smoke.log
+fi
+if want bench; then
+  timeout -k 10 400 python bench.py --json-out $O/bench_fluA.json > $O/bench_fluA.log 2>&1
+  tail -c 1500 $O/bench_fluA.json
+fi
+if want shard8; then
+  timeout -k 10 300 python bench.py --workload synthetic --shard-of 8 --steps 100 --warmup 10 \
+    --no-cpu-baseline --json-out $O/bench_shard8.json > $O/bench_shard8.log 2>&1
+  python -c "import json;d=json.load(open('$O/bench_shard8.json'));print('shard8', d['value'], d['ms_per_step'])"
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof_shard8 -o run -- \
+    python bench.py --workload synthetic --shard-of 8 --steps 50 --warmup 5 --no-cpu-baseline \
+    > $O/prof_shard8.log 2>&1
+fi
+if want synth; then
+  timeout -k 10 300 python bench.py --workload synthetic --steps 50 --warmup 5 --no-cpu-baseline \
+    --json-out $O/bench_synth.json > $O/bench_synth.log 2>&1
+  python -c "import json;d=json.load(open('$O/bench_synth.json'));print('synth', d['value'], d['ms_per_step'])"
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof_synth -o run -- \
+    python bench.py --workload synthetic --steps 30 --warmup 5 --no-cpu-baseline > $O/prof_synth.log 2>&1
+fi
+if want multidev; then
+  timeout -k 10 300 python bench.py --workload synthetic --multi-device 1 --steps 30 --warmup 5 \
+    --no-cpu-baseline --json-out $O/bench_multidev1.json > $O/bench_multidev1.log 2>&1
+  python -c "import json;d=json.load(open('$O/bench_multidev1.json'));print('multidev1', d['value'], d['config']['parallelism'])"
+fi
+if want prof; then
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof_fluA -o run -- \
+    python bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-sampler-latency > $O/prof_fluA.log 2>&1
+fi
+if want lat; then
+  timeout -k 10 300 python tools/latency_probe.py > $O/latency.log 2>&1
+  tail -20 $O/latency.log
+fi
+echo done

@@ -4,7 +4,7 @@ for the GPU: the time per gradient round minus the stand-in's own time is
 what the sampler, transforms, priors and chain rule cost per round.
 
 Test infrastructure (it calls oracle/): run from the repository root as
-    python -m tests.host_overhead [--warmup 60 --samples 60 --profile]
+    python -m tools.host_overhead [--warmup 60 --samples 60 --profile]
 """
 import argparse
 import cProfile
