@@ -2298,19 +2298,16 @@ int launch_class(phy_ctx* ctx, int n, const double* d_blens, const double* d_mod
     a.count = L.nchunk;
     hipLaunchKernelGGL(cls_fwd_kernel, dim3((L.nchunk + 3) / 4, dcn), dim3(256), 0, st, a);
   }
-  hipLaunchKernelGGL(cls_root_ll_kernel, dim3((e->nroot + 255) / 256, n), dim3(256), 0, st, a);
-  hipLaunchKernelGGL(cls_root_rev_kernel, dim3(e->nrootch, dcn), dim3(64), 0, st, a);
+  if (C <= 4)
+    hipLaunchKernelGGL(cls_root_kernel<256>, dim3(e->nrootch, n), dim3(C * WAVE), 0, st, a);
+  else
+    hipLaunchKernelGGL(cls_root_kernel<1024>, dim3(e->nrootch, n), dim3(C * WAVE), 0, st, a);
   for (int l = e->levels - 1; l > e->Lc; --l) {
     const ClassLevel& L = e->lv[l];
     if (L.ntile) {
       a.first = L.tile0;
       a.count = L.ntile;
       hipLaunchKernelGGL(cls_red_kernel, dim3((L.ntile + 3) / 4, dcn), dim3(256), 0, st, a);
-    }
-    if (L.nspan && !L.fixed_in_rev) {  // else summed by the REV waves of the spans' chunks
-      a.first = L.span0;
-      a.count = L.nspan;
-      hipLaunchKernelGGL(cls_fix_kernel, dim3((L.nspan + 3) / 4, dcn), dim3(256), 0, st, a);
     }
     if (L.nchunk) {
       a.first = L.chunk0;
@@ -2322,9 +2319,6 @@ int launch_class(phy_ctx* ctx, int n, const double* d_blens, const double* d_mod
     if (e->nrtile)
       hipLaunchKernelGGL(cls_red_list_kernel, dim3((e->nrtile + 3) / 4, dcn), dim3(256), 0, st, a,
                          (const int*)e->d_rtile, e->nrtile);
-    if (e->nrspan)
-      hipLaunchKernelGGL(cls_fix_list_kernel, dim3((e->nrspan + 3) / 4, dcn), dim3(256), 0, st, a,
-                         (const int*)e->d_rspan, e->nrspan);
     hipLaunchKernelGGL(cls_clade_rev_kernel, dim3(e->nclade, dcn), dim3(CLADE_THREADS), 0, st, a,
                        (const CladeLevel*)e->d_clade, e->Lc);
   }
