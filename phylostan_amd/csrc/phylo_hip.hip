@@ -2324,20 +2324,15 @@ int launch_class(phy_ctx* ctx, int n, const double* d_blens, const double* d_mod
   }
   HIP_TRY(hipGetLastError());
   if (ctx->timing) HIP_TRY(hipEventRecord(e1, st));
-  if (e->max_gcount > 64)
-    hipLaunchKernelGGL(cls_gsum_kernel, dim3(B, dcn), dim3(1024), 0, st, (const double*)e->d_gpart,
-                       (const int*)e->d_gbase, (const int*)e->d_gcount, grows, gstride, B, C, std::max(e->ngs, 1));
-  else
-    hipLaunchKernelGGL(cls_gsum_small_kernel, dim3((unsigned)(((long long)dcn * B * 16 + 255) / 256)), dim3(256), 0,
-                       st, (const double*)e->d_gpart, (const int*)e->d_gbase, (const int*)e->d_gcount, grows, gstride,
-                       B, C, std::max(e->ngs, 1), dcn);
   if (d_site)
     hipLaunchKernelGGL(cls_site_kernel, dim3((ctx->P + 255) / 256, n), dim3(256), 0, st,
                        (const double*)e->d_sitecls, (const int*)e->d_pat_root, d_site, ctx->P, e->nroot);
-  FinArgs fa{ctx->d_gslot, e->d_sslot, ctx->d_pmat, ctx->eig_cur, d_blens, d_model, ctx->d_gpos, ctx->d_inner, d_out,
-             C,            B,          ctx->nmat,   e->nrootch,  phy_output_len(ctx), 0, ctx->R, grows, gstride,
-             ctx->kind,    0,          ctx->qfuse_pref ? 1 : 0};
-  *qdone = launch_finalize(fa, n, st);
+  double* epi = e->d_epi;
+  EpiArgs ea{e->d_gpart, e->d_gbase, e->d_gcount, e->d_sslot, ctx->d_pmat, ctx->eig_cur, d_blens, d_model,
+             ctx->d_gpos, grows, gstride, d_out, epi, epi + (size_t)n * C * B, epi + (size_t)n * (C * B + 16 * B),
+             e->d_epicnt, C, B, ctx->nmat, ctx->R, std::max(e->ngs, 1), e->nrootch, phy_output_len(ctx), ctx->kind};
+  hipLaunchKernelGGL(cls_epi_kernel, dim3(B, n), dim3(EPI_THREADS), 0, st, ea);
+  *qdone = true;
   HIP_TRY(hipGetLastError());
   return PHY_OK;
 }
