@@ -324,7 +324,134 @@ def mixture_fixture(phylo, specs):
     return out
 
 
+def _pattern_alignment(layout, taxa):
+    """The dataset's compressed patterns as an alignment object in the
+    reference pruner's input form (one column per pattern; tip masks back to
+    symbols: A C G T, '-' for the all-ones mask; the fixtures hold only
+    one-hot and all-ones masks), plus the pattern weights."""
+    sym = {1: "A", 2: "C", 4: "G", 8: "T", 15: "-"}
+    tb = layout["tipbits"]
+    assert set(np.unique(tb).tolist()) <= set(sym), "unexpected tip mask in the fixture"
+    rows = {t: _Seq("".join(sym[int(v)] for v in tb[k])) for k, t in enumerate(taxa)}
+    return _Alignment(rows), np.asarray(layout["weights"], dtype=np.float64)
+
+
+def _ref_mixture_loglik(phylo, tree, alignment, weights, blens, rates, freqs, rs, ps, merged=None):
+    """sum_i w_i log sum_c ps_c L_c,i with every L_c,i from the reference's
+    scripts/phylo.py pruner (:240-296) on edges blens[node index] * r_c (the
+    mixture line generate_script.py:1006-1010 restated); `merged`: the node
+    whose edge is 0 (DS1's merged root branch, generate_script.py:1019)."""
+    lik = 0.0
+    for c in range(len(rs)):
+        for nd in tree.postorder_node_iter():
+            if nd.parent_node is not None:
+                nd.edge_length = 0.0 if nd.index == merged else float(blens[nd.index]) * float(rs[c])
+        lik = lik + float(ps[c]) * _phylo_root_site_lik(phylo, tree, alignment, phylo.GTR(list(rates), list(freqs)))
+    return float(np.dot(weights, np.log(lik)))
+
+
+GRAD_BRANCHES = 10  # branch-length derivatives per config point (spread over tip and internal branches)
+
+
+def grad_fixture(phylo, specs):
+    """Central differences of the reference's own likelihood (scripts/phylo.py
+    pruner, mixture per generate_script.py:1006-1010) at the three configs'
+    points: d/dblens for GRAD_BRANCHES branches, d/dkappa (fluA HKY) or the
+    six GTR exchangeabilities (HCV), the four frequencies (as free
+    variables: phylo.GTR uses them as given, so does the emitted Stan model,
+    generate_script.py:855-868), and the Weibull shape through rs
+    (:267-278).  Each derivative is Richardson-extrapolated from steps h and
+    h/2 (truncation O(h^4)); the tests compare at rel 1e-6."""
+    from phylostan_amd import models
+    out = {"source": "central differences (Richardson, steps h and h/2) of scripts/phylo.py:240-296 "
+                     "(per category) combined as generate_script.py:1006-1010", "points": []}
+
+    def deriv(f, x0, h):
+        d1 = (f(x0 + h) - f(x0 - h)) / (2 * h)
+        d2 = (f(x0 + h / 2) - f(x0 - h / 2)) / h
+        return (4.0 * d2 - d1) / 3.0
+
+    with open(os.path.join(HERE, "phylo_mixture.json")) as fp:
+        mix = {p["dataset"]: p for p in json.load(fp)["points"]}
+    for name in ("fluA", "HCV", "DS1"):
+        pt = mix[name]
+        tpath, apath = specs[name][:2]
+        layout = np.load(os.path.join(HERE, "%s_layout.npz" % name), allow_pickle=False)
+        tree = treeio.read_tree(tpath)
+        tree.resolve_polytomies(update_bipartitions=True)
+        aln = treeio.read_alignment(apath)
+        full = _Alignment({t.label: _Seq(aln[t.label]) for t in tree.taxon_namespace})
+        phylo.setup_indexes(tree, full)
+        taxa = [t.label for t in tree.taxon_namespace]
+        alignment, w = _pattern_alignment(layout, taxa)
+        S = len(taxa)
+        merged = None if pt["rooted"] else 2 * S - 3
+        blens = np.array(pt["blens"], dtype=np.float64)
+        B = blens.size
+        rates, freqs = list(pt["rates"]), list(pt["freqs"])
+        rs, ps = list(pt["rs"]), list(pt["ps"])
+
+        def F(bl=None, rt=None, fq=None, rsv=None):
+            return _ref_mixture_loglik(phylo, tree, alignment, w, blens if bl is None else bl,
+                                       rates if rt is None else rt, freqs if fq is None else fq,
+                                       rs if rsv is None else rsv, ps, merged)
+
+        ll0 = F()
+        assert abs(ll0 - pt["loglik"]) <= 1e-9 * abs(pt["loglik"]), (ll0, pt["loglik"])
+        rec = {"dataset": name, "model": pt["model"], "rooted": pt["rooted"], "C": pt["C"], "loglik": ll0}
+        br = np.unique(np.linspace(0, B - 1, GRAD_BRANCHES).round().astype(int)).tolist()
+        gb = []
+        for b in br:
+            h = 1e-3 * max(blens[b], 1e-4)
+
+            def fb(x, b=b):
+                bl = blens.copy()
+                bl[b] = x
+                return F(bl=bl)
+            gb.append(deriv(fb, blens[b], h))
+        rec["branches"] = br
+        rec["grad_blens"] = gb
+        if pt["model"] == "HKY":
+            kappa = rates[1]
+            rec["kappa"] = kappa
+            rec["grad_kappa"] = deriv(lambda k: F(rt=[1.0, k, 1.0, 1.0, k, 1.0]), kappa, 1e-3 * kappa)
+        if pt["model"] == "GTR":
+            gr = []
+            for k in range(6):
+                def fr(x, k=k):
+                    rt = list(rates)
+                    rt[k] = x
+                    return F(rt=rt)
+                gr.append(deriv(fr, rates[k], 1e-3 * rates[k]))
+            rec["grad_rates"] = gr
+        if pt["model"] != "JC69":
+            gf = []
+            for k in range(4):
+                def ff(x, k=k):
+                    fq = list(freqs)
+                    fq[k] = x
+                    return F(fq=fq)
+                gf.append(deriv(ff, freqs[k], 1e-4 * freqs[k]))
+            rec["grad_freqs"] = gf
+        if pt["C"] > 1:
+            shape = pt["wshape"]
+            rec["wshape"] = shape
+            rec["grad_wshape"] = deriv(lambda a: F(rsv=list(models.weibull_site_rates(a, pt["C"])[0])), shape,
+                                       1e-3 * shape)
+        out["points"].append(rec)
+        print(name, "reference FD gradients:", {k: v for k, v in rec.items() if k.startswith("grad")})
+    return out
+
+
 def main():
+    if len(sys.argv) > 1 and sys.argv[1] == "grad":  # only the reference FD gradients
+        ex = os.path.join(REF, "examples")
+        specs = {"fluA": (os.path.join(ex, "fluA", "fluA.tree"), os.path.join(ex, "fluA", "fluA.fa")),
+                 "HCV": (os.path.join(ex, "HCV", "HCV.tree"), os.path.join(ex, "HCV", "HCV.nexus")),
+                 "DS1": (os.path.join(ex, "DS1", "DS1.trees"), os.path.join(ex, "DS1", "DS1.nex"))}
+        with open(os.path.join(HERE, "phylo_grad.json"), "w") as fp:
+            json.dump(grad_fixture(_import_reference_phylo(), specs), fp, indent=1)
+        return
     if len(sys.argv) > 1 and sys.argv[1] == "mixture":  # only the mixture / unrooted fixture
         ex = os.path.join(REF, "examples")
         specs = {"fluA": (os.path.join(ex, "fluA", "fluA.tree"), os.path.join(ex, "fluA", "fluA.fa")),

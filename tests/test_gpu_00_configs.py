@@ -132,6 +132,29 @@ def test_config_vs_reference_pruner(k):
                          e_ref_site, fmt(e), eq))
 
 
+@pytest.mark.parametrize("k", range(3), ids=["fluA_HKY_W4", "HCV_GTR_W4", "DS1_JC69_unrooted"])
+def test_config_gradients_vs_reference_fd(k):
+    """a9 pinned to the reference itself: the GPU's gradients (branch lengths,
+    kappa or the six GTR exchangeabilities, the frequencies through Q plus the
+    root term, the Weibull shape through dlogL/drs) against central
+    differences of the reference's own likelihood (scripts/phylo.py per
+    category, the mixture of generate_script.py:1006-1010;
+    tests/golden/phylo_grad.json) at rel 1e-6, on both engines."""
+    from tests.test_oracle import REF_GRAD_RTOL, reference_grad_errors, reference_grad_points
+    pt = reference_grad_points()[k]
+    mp = [p for p in cases.load_mixture_points() if p["dataset"] == pt["dataset"]][0]
+    case = cases.mixture_case(mp)
+    for engine in ("pattern", "class"):
+        eng = _engine(case)
+        eng.set_engine(engine)
+        res = eng.evaluate(case.blens, case.model_vec())
+        errs = reference_grad_errors({"grad_blens": res.grad_blens, "grad_rs": res.grad_rs,
+                                      "grad_rates": res.grad_rates, "grad_freqs": res.grad_freqs}, pt, case)
+        assert all(v <= REF_GRAD_RTOL for v in errs.values()), (engine, errs)
+        report.record("%s [%s]: gradients vs reference finite differences: %s"
+                      % (MIXTURE_IDS[pt["dataset"]], engine, "  ".join("%s %.1e" % kv for kv in errs.items())))
+
+
 @pytest.mark.parametrize("k", range(4))
 def test_reference_phylo_py_points(k):
     """HKY / GTR (C = 1) through the eigen path against scripts/phylo.py."""

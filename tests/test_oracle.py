@@ -7,6 +7,7 @@
 * HKY / GTR P-matrices vs scipy.linalg.expm (the Stan Math eigen path is
   absent here: parity unpinned by the reference, pinned to expm instead).
 """
+import os
 import numpy as np
 import pytest
 import scipy.linalg
@@ -227,3 +228,57 @@ def test_oracle_vs_reference_mixture_and_unrooted(k):
                            case.model_vec(), case.blens, case.C, site_ll=True)
     np.testing.assert_allclose(sl, pt["site_ll"], rtol=1e-10, atol=1e-12)
     assert abs(out[0] - pt["loglik"]) <= 1e-10 * abs(pt["loglik"])
+
+
+def reference_grad_points():
+    """tests/golden/phylo_grad.json: central differences (Richardson) of the
+    reference's own scripts/phylo.py likelihood, the mixture combined as
+    generate_script.py:1006-1010 (tests/golden/make_golden.py grad_fixture)."""
+    import json
+    with open(os.path.join(cases.GOLDEN, "phylo_grad.json")) as fp:
+        return json.load(fp)["points"]
+
+
+def reference_grad_errors(res_like, pt, case):
+    """Max relative errors of an evaluation's gradients against the reference
+    FD point: res_like has grad_blens, grad_rs, grad_rates, grad_freqs."""
+    from phylostan_amd import models
+    errs = {}
+    gb = np.asarray(res_like["grad_blens"])[pt["branches"]]
+    ref = np.asarray(pt["grad_blens"])
+    errs["blens"] = float(np.max(np.abs(gb - ref) / np.maximum(np.abs(ref), 1e-3 * np.max(np.abs(ref)))))
+    if "grad_kappa" in pt:
+        k = models.kappa_gradient(np.asarray(res_like["grad_rates"]))
+        errs["kappa"] = abs(k - pt["grad_kappa"]) / abs(pt["grad_kappa"])
+    if "grad_rates" in pt:
+        r = np.asarray(pt["grad_rates"])
+        errs["rates"] = float(np.max(np.abs(np.asarray(res_like["grad_rates"]) - r)) / np.max(np.abs(r)))
+    if "grad_freqs" in pt:
+        f = np.asarray(pt["grad_freqs"])
+        errs["freqs"] = float(np.max(np.abs(np.asarray(res_like["grad_freqs"]) - f)) / np.max(np.abs(f)))
+    if "grad_wshape" in pt:
+        dr = models.weibull_site_rates_dshape(pt["wshape"], case.C)
+        ga = float(np.dot(np.asarray(res_like["grad_rs"]), dr))
+        errs["wshape"] = abs(ga - pt["grad_wshape"]) / abs(pt["grad_wshape"])
+    return errs
+
+
+REF_GRAD_RTOL = 1e-6  # finite differences of the reference (Richardson, h/x = 1e-3 / 1e-4)
+
+
+@pytest.mark.parametrize("k", range(3), ids=["fluA_HKY_W4", "HCV_GTR_W4", "DS1_JC69_unrooted"])
+def test_oracle_gradients_vs_reference_fd(k):
+    """The oracle's analytic gradients (branch lengths, kappa or the GTR
+    exchangeabilities, frequencies, Weibull shape through rs) against central
+    differences of the reference's own likelihood (scripts/phylo.py)."""
+    from phylostan_amd import models
+    pt = reference_grad_points()[k]
+    mp = [p for p in cases.load_mixture_points() if p["dataset"] == pt["dataset"]][0]
+    case = cases.mixture_case(mp)
+    ref = case.oracle()
+    assert abs(ref["loglik"] - pt["loglik"]) <= 1e-10 * abs(pt["loglik"])
+    gr, gf = models.q_param_gradients(ref["dLdP"], case.blens, case.rs, case.freqs, case.rates,
+                                      ref["grad_freq_root"])
+    errs = reference_grad_errors({"grad_blens": ref["grad_blens"], "grad_rs": ref["grad_rs"], "grad_rates": gr,
+                                  "grad_freqs": gf}, pt, case)
+    assert all(v <= REF_GRAD_RTOL for v in errs.values()), errs
