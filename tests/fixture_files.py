@@ -35,7 +35,30 @@ def _newick(peel1, taxa, height, S):
     return "(%s,%s);" % (rec(a, height[root]), rec(b, height[root]))
 
 
-def write_dataset(name, outdir):
+def _newick_trifurcating(peel1, taxa, S):
+    """An unrooted fixture's tree as the reference ships it (examples/DS1/
+    DS1.trees): no branch lengths, a trifurcating root (c1, x, y) where the
+    resolved root row is (c1, 2S-2, root) and node 2S-2 (1-based) = (x, y) --
+    reading it back and resolving the polytomy (phylostan.py:175) gives the
+    fixture's node numbering again."""
+    kids = {int(v): (int(a), int(b)) for a, b, v in peel1}
+    root = int(peel1[-1][2])
+
+    def rec(v):
+        if v <= S:
+            return taxa[v - 1]
+        a, b = kids[v]
+        return "(%s,%s)" % (rec(a), rec(b))
+
+    c1, n = kids[root]
+    assert n == 2 * S - 2, "the resolved root's second child must be node 2S-2 (1-based)"
+    x, y = kids[n]
+    return "(%s,%s,%s);" % (rec(c1), rec(x), rec(y))
+
+
+def write_dataset(name, outdir, reference_form=False):
+    """reference_form (unrooted datasets): the tree file in the reference's
+    own form -- trifurcating root, no branch lengths (DS1.trees)."""
     d = cases.load_layout(name)
     S = d["tipbits"].shape[0]
     taxa = [str(t) for t in d["taxa"]]
@@ -48,7 +71,10 @@ def write_dataset(name, outdir):
             height[v] = max(height[a], height[b]) + 0.05
     tree_path = os.path.join(outdir, name + ".tree")
     with open(tree_path, "w") as fp:
-        fp.write(_newick(d["peel"], taxa, height, S) + "\n")
+        if reference_form and "heights" not in d:
+            fp.write(_newick_trifurcating(d["peel"], taxa, S) + "\n")
+        else:
+            fp.write(_newick(d["peel"], taxa, height, S) + "\n")
     codes = d["tipbits"]
     w = d["weights"].astype(int)
     cols = np.repeat(np.arange(codes.shape[1]), w)

@@ -266,3 +266,20 @@ def test_parse_reroots_a_multifurcating_root_like_the_reference():
     t3.reroot_at_edge(t3.seed_node.child_nodes()[0].edge)
     kids = t3.seed_node.child_nodes()
     assert kids[0].taxon.label == "a" and [c.taxon.label for c in kids[1].child_nodes()] == ["b", "c", "d"]
+
+
+def test_ds1_reference_form_tree_round_trips(tmp_path):
+    """The DS1 fixture written as the reference ships its trees (trifurcating
+    root, no branch lengths: examples/DS1/DS1.trees) loads back, through the
+    CLI's unrooted path (no --clock), to the fixture's peel and map -- the
+    layout tests/test_data_prep.py pins to phylostan/utils.py."""
+    from phylostan_amd import data as dataio
+    from tests import cases
+    t, a = fixture_files.write_dataset("DS1", str(tmp_path), reference_form=True)
+    text = open(t).read()
+    assert ":" not in text and text.count(",") == 26
+    d = dataio.load(t, a, rooted=False, heterochronous=False)
+    lay = cases.load_layout("DS1")
+    np.testing.assert_array_equal(d.peel0, lay["peel"] - 1)
+    np.testing.assert_array_equal(d.tipcodes, lay["tipbits"])
+    np.testing.assert_array_equal(d.weights, lay["weights"])

@@ -137,3 +137,39 @@ def test_fluA_fullrank_advi_runs_to_convergence(tmp_path):
     for key, (lo, hi) in README_CI.items():
         m = res[key][0]
         assert lo <= m <= hi, "%s mean %g outside the reference's 95%% CI (%g, %g)" % (key, m, lo, hi)
+
+
+def test_config1_ds1_jc69_unrooted_meanfield(tmp_path, capsys):
+    """BASELINE config 1 as the reference runs it (examples/SConstruct:170-188,
+    run_stan :71-88): `phylostan build -m JC69`, then `phylostan run -i DS1 -t
+    tree0 -s jc69.stan -o tree0 -m JC69 --eta 0.1` -- no clock, so the
+    unrooted model with the root branch merged (generate_script.py:1013-1023)
+    and blens ~ exponential(10) (:1404) -- on DS1 and its first tree in the
+    reference's form (trifurcating root, no branch lengths), every gradient
+    from the GPU engine.  The posterior is parity-unpinned (the reference
+    publishes no DS1 numbers); this checks the run's contract: Stan's progress
+    lines (the regex SConstruct:128 parses), an ELBO that rises and stops by
+    tol_rel_obj, `blens.k` columns, and `parse` giving the .trees file `run`
+    wrote (same node numbering for the trifurcating root)."""
+    import re
+    from phylostan_amd import cli, stan_io
+    t, a = fixture_files.write_dataset("DS1", str(tmp_path), reference_form=True)
+    script = str(tmp_path / "jc69.stan")
+    assert cli.main(["build", "-m", "JC69", "-s", script]) == 0
+    out = str(tmp_path / "tree0")
+    capsys.readouterr()
+    cli.main(["run", "-i", a, "-t", t, "-s", script, "-o", out, "-m", "JC69", "--eta", "0.1", "--seed", "1"])
+    printed = capsys.readouterr().out
+    prog = [(int(m.group(1)), float(m.group(2))) for m in re.finditer(r"\s+(\d+)\s+(-\d+\.\d+)", printed)]
+    assert len(prog) >= 5, printed[:2000]
+    elbo = np.array([e for _, e in prog])
+    assert np.isfinite(elbo).all() and elbo[-1] > elbo[0] + 1000.0
+    assert "ELBO CONVERGED" in printed and prog[-1][0] < 100000
+    header, data = stan_io.read_samples(out)
+    B = 2 * 27 - 3
+    assert header[:B + 1] == ["lp__"] + ["blens.%d" % k for k in range(1, B + 1)]
+    assert data.shape == (1001, len(header)) and np.isfinite(data).all() and np.all(data[:, 1:B + 1] > 0)
+    cli.main(["parse", "--samples", out, "-t", t, "-o", str(tmp_path / "parsed.trees")])
+    ran = open(out + ".trees").read()
+    parsed = open(str(tmp_path / "parsed.trees")).read()
+    assert ran.count("tree ") == 1001 and ran == parsed
