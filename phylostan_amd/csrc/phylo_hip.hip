@@ -2282,7 +2282,7 @@ int launch_class(phy_ctx* ctx, int n, const double* d_blens, const double* d_mod
   ClassEngine* e = ctx->ce;
   const int C = ctx->C, B = ctx->B;
   if ((long)n * C > 65535) return fail(PHY_ERANGE, "class sweep: n_draws * C must be <= 65535");
-  int rc = class_engine_reserve(e, n);
+  int rc = class_engine_reserve(e, n, st);
   if (rc) return rc;
   ClassArgs a = class_args(e, ctx->d_pmat, d_model, ctx->extra);
   const int dcn = n * C;
@@ -2445,7 +2445,7 @@ int launch_graphed(phy_ctx* ctx, int n, const void* bl, const void* md, const vo
   {
     int rc = PHY_OK;
     if (ctx->engine == 1 && n > ctx->ce->max_draws) {
-      if ((rc = class_engine_reserve(ctx->ce, n))) return rc;
+      if ((rc = class_engine_reserve(ctx->ce, n, st))) return rc;
       ++ctx->plan_gen;
     } else if (ctx->engine == 2 && n > ctx->re->max_draws) {
       if ((rc = res_engine_reserve(ctx->re, n))) return rc;
