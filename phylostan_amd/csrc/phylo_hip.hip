@@ -1422,6 +1422,121 @@ __host__ __device__ void eig_record(const double* mdl, int kind, double* out) {
   }
 }
 
+// eig_record for one wave (pmat_kernel<true>: a small device batch, where
+// the one-lane chain of eig_record was most of the launch): lane (j, k),
+// j, k < 4, owns element [j][k] of Q, A and V; the Jacobi rotation
+// parameters are formed by every lane from the same LDS values, each pass of
+// a round updates the 16 elements in parallel through LDS.  Every element
+// sees exactly eig_record's operations in eig_record's order (no FMA
+// contraction), so the record is bitwise eig_record's (tested against the
+// host-formed eigensystems).  All 64 lanes must call it; `sh` is 48 doubles
+// of LDS; the result lands in `out` (LDS, EIG_LEN doubles).
+__device__ void eig_record_wave(const double* mdl, int kind, double* out, double* sh, int lane) {
+#pragma clang fp contract(off)
+  const int j = (lane >> 2) & 3, k = lane & 3;
+  const bool own = lane < 16;
+  double* A = sh;       // [4][4]
+  double* V = sh + 16;  // [4][4]
+  double* T = sh + 32;  // scratch [4][4]
+  if (kind == PHY_JC69) {
+    if (own) out[EIG_Q + j * 4 + k] = (j == k) ? -1.0 : 1.0 / 3.0;
+    __syncthreads();
+    return;
+  }
+  const double f[4] = {mdl[0], mdl[1], mdl[2], mdl[3]};
+  const double* r = mdl + 4;
+  const double R[4][4] = {{0.0, r[0], r[1], r[2]}, {r[0], 0.0, r[3], r[4]}, {r[1], r[3], 0.0, r[5]},
+                          {r[2], r[4], r[5], 0.0}};
+  // Q = R diag(pi) with zero-sum rows and the normaliser s, in eig_record's
+  // order (every lane: a few dozen operations)
+  double q[4][4];
+  double sn = 0.0;
+#pragma unroll
+  for (int jj = 0; jj < 4; ++jj) {
+    double row = 0.0;
+#pragma unroll
+    for (int kk = 0; kk < 4; ++kk) {
+      q[jj][kk] = (jj == kk) ? 0.0 : R[jj][kk] * f[kk];
+      row += q[jj][kk];
+    }
+    q[jj][jj] = -row;
+    sn -= q[jj][jj] * f[jj];
+  }
+  double sq[4];
+#pragma unroll
+  for (int jj = 0; jj < 4; ++jj) sq[jj] = sqrt(f[jj]);
+  // this lane's element: q[j][k] / s, q[k][j] / s, then A[j][k]
+  double qjk = 0.0, qkj = 0.0;
+#pragma unroll
+  for (int jj = 0; jj < 4; ++jj)
+#pragma unroll
+    for (int kk = 0; kk < 4; ++kk) {
+      if (jj == j && kk == k) qjk = q[jj][kk];
+      if (jj == k && kk == j) qkj = q[jj][kk];
+    }
+  qjk /= sn;
+  qkj /= sn;
+  const double sqj = j == 0 ? sq[0] : j == 1 ? sq[1] : j == 2 ? sq[2] : sq[3];
+  const double sqk = k == 0 ? sq[0] : k == 1 ? sq[1] : k == 2 ? sq[2] : sq[3];
+  if (own) {
+    out[EIG_Q + j * 4 + k] = qjk;
+    A[j * 4 + k] = (j == k) ? qjk : 0.5 * (sqj * qjk / sqk + sqk * qkj / sqj);
+    V[j * 4 + k] = (j == k) ? 1.0 : 0.0;
+  }
+  if (lane == 0) out[EIG_S] = sn;
+  __syncthreads();
+  for (int sweep = 0; sweep < 50; ++sweep) {
+    double off = 0.0, tot = 0.0;
+    for (int i = 0; i < 4; ++i)
+      for (int jj = 0; jj < 4; ++jj) {
+        tot += A[i * 4 + jj] * A[i * 4 + jj];
+        if (i != jj) off += A[i * 4 + jj] * A[i * 4 + jj];
+      }
+    if (off <= 1e-32 * tot || off == 0.0) break;  // wave-uniform
+#pragma unroll
+    for (int rr = 0; rr < 3; ++rr) {
+      const int p1 = 0, q1 = rr + 1;
+      const int p2 = rr == 0 ? 2 : 1, q2 = rr == 2 ? 2 : 3;
+      double c1, s1, c2, s2;
+      jacobi_rot(A[p1 * 4 + p1], A[q1 * 4 + q1], A[p1 * 4 + q1], c1, s1);
+      jacobi_rot(A[p2 * 4 + p2], A[q2 * 4 + q2], A[p2 * 4 + q2], c2, s2);
+      // element (j, k)'s rotation: the pair {p, q} holding k (columns) / j (rows)
+      auto rot = [&](const double* M, int row, int col, bool by_col) __attribute__((always_inline)) -> double {
+        const int x = by_col ? col : row;
+        const bool first = x == p1 || x == q1;
+        const int p = first ? p1 : p2, qq = first ? q1 : q2;
+        const double cc = first ? c1 : c2, ss = first ? s1 : s2;
+        const double av = by_col ? M[row * 4 + p] : M[p * 4 + col];
+        const double bv = by_col ? M[row * 4 + qq] : M[qq * 4 + col];
+        return x == p ? cc * av - ss * bv : ss * av + cc * bv;
+      };
+      double na = 0.0, nv = 0.0;
+      if (own) {
+        na = rot(A, j, k, true);   // A <- A J (columns)
+        nv = rot(V, j, k, true);   // V <- V J
+        T[j * 4 + k] = na;
+      }
+      __syncthreads();
+      if (own) {
+        na = rot(T, j, k, false);  // A <- J^T A (rows)
+        if ((j == p1 && k == q1) || (j == q1 && k == p1) || (j == p2 && k == q2) || (j == q2 && k == p2)) na = 0.0;
+      }
+      __syncthreads();
+      if (own) {
+        A[j * 4 + k] = na;
+        V[j * 4 + k] = nv;
+      }
+      __syncthreads();
+    }
+  }
+  if (own) {
+    if (k == 0) out[EIG_LAM + j] = A[j * 4 + j];
+    out[EIG_M1 + j * 4 + k] = V[j * 4 + k] / sqj;  // Pi^-1/2 V
+    out[EIG_M2 + j * 4 + k] = V[k * 4 + j] * sqk;  // V^T Pi^1/2
+  }
+  __syncthreads();
+}
+
 // One thread per draw.
 __global__ void __launch_bounds__(64) eig_kernel(PmatArgs a) {
   const int draw = blockIdx.x * blockDim.x + threadIdx.x;
@@ -1449,12 +1564,10 @@ __global__ void __launch_bounds__(64) pmat_kernel(PmatArgs a) {
   const int draw = blockIdx.y;
   const int C = a.C, nmat = a.nmat;
   const int lane = threadIdx.x;
-  if constexpr (WITH_EIG) {  // a serial chain of one thread: every wave of the draw forms it (no eig launch)
-    if (lane == 0) {
-      eig_record(a.model + (size_t)draw * (10 + 2 * C), a.kind, e);
-      if (blockIdx.x == 0)
-        for (int k = 0; k < EIG_LEN; ++k) a.eig[(size_t)draw * EIG_LEN + k] = e[k];
-    }
+  if constexpr (WITH_EIG) {  // every wave of the draw forms it, lane-parallel (no eig launch)
+    __shared__ double esh[48];
+    eig_record_wave(a.model + (size_t)draw * (10 + 2 * C), a.kind, e, esh, lane);
+    if (blockIdx.x == 0 && lane < EIG_LEN) a.eig[(size_t)draw * EIG_LEN + lane] = e[lane];
   } else if (lane < EIG_LEN) {
     e[lane] = a.eig[(size_t)draw * EIG_LEN + lane];
   }
@@ -2309,6 +2422,11 @@ int launch_class(phy_ctx* ctx, int n, const double* d_blens, const double* d_mod
       a.count = L.ntile;
       hipLaunchKernelGGL(cls_red_kernel, dim3((L.ntile + 3) / 4, dcn), dim3(256), 0, st, a);
     }
+    if (L.nspan && !e->tickets) {
+      a.first = L.span0;
+      a.count = L.nspan;
+      hipLaunchKernelGGL(cls_fix_kernel, dim3((L.nspan + 3) / 4, dcn), dim3(256), 0, st, a);
+    }
     if (L.nchunk) {
       a.first = L.chunk0;
       a.count = L.nchunk;
@@ -2319,6 +2437,9 @@ int launch_class(phy_ctx* ctx, int n, const double* d_blens, const double* d_mod
     if (e->nrtile)
       hipLaunchKernelGGL(cls_red_list_kernel, dim3((e->nrtile + 3) / 4, dcn), dim3(256), 0, st, a,
                          (const int*)e->d_rtile, e->nrtile);
+    if (e->nrspan && !e->tickets)
+      hipLaunchKernelGGL(cls_fix_list_kernel, dim3((e->nrspan + 3) / 4, dcn), dim3(256), 0, st, a,
+                         (const int*)e->d_rspan, e->nrspan);
     hipLaunchKernelGGL(cls_clade_rev_kernel, dim3(e->nclade, dcn), dim3(CLADE_THREADS), 0, st, a,
                        (const CladeLevel*)e->d_clade, e->Lc);
   }
@@ -2328,10 +2449,11 @@ int launch_class(phy_ctx* ctx, int n, const double* d_blens, const double* d_mod
     hipLaunchKernelGGL(cls_site_kernel, dim3((ctx->P + 255) / 256, n), dim3(256), 0, st,
                        (const double*)e->d_sitecls, (const int*)e->d_pat_root, d_site, ctx->P, e->nroot);
   double* epi = e->d_epi;
+  const size_t ncb = (size_t)n * C * B;
   EpiArgs ea{e->d_gpart, e->d_gbase, e->d_gcount, e->d_sslot, ctx->d_pmat, ctx->eig_cur, d_blens, d_model,
-             ctx->d_gpos, grows, gstride, d_out, epi, epi + (size_t)n * C * B, epi + (size_t)n * (C * B + 16 * B),
+             ctx->d_gpos, grows, gstride, d_out, epi, epi + ncb, epi + 17 * ncb,
              e->d_epicnt, C, B, ctx->nmat, ctx->R, std::max(e->ngs, 1), e->nrootch, phy_output_len(ctx), ctx->kind};
-  hipLaunchKernelGGL(cls_epi_kernel, dim3(B, n), dim3(EPI_THREADS), 0, st, ea);
+  hipLaunchKernelGGL(cls_epi_kernel, dim3(C * B, n), dim3(EPI_THREADS), 0, st, ea);
   *qdone = true;
   HIP_TRY(hipGetLastError());
   return PHY_OK;
