@@ -1278,6 +1278,8 @@ __global__ void __launch_bounds__(MAXT) __attribute__((amdgpu_waves_per_eu(MAXT 
   }
 }
 
+#include "quad_engine.inc"
+
 // ---------------------------------------------------------------------------
 // P-matrices (generate_script.py:755-892)
 // ---------------------------------------------------------------------------
@@ -1871,6 +1873,13 @@ struct phy_ctx {
   int K = 1;                   // columns per lane of the current plan
   bool klat = false;           // K = 1 latency plan (sweep_kernel<512, 1, .>: no register spills)
   bool klat_pref = true;       // PHY_KLAT=0: the latency plan keeps the four-wave K = 1 kernel
+  // the quad sweep (quad_engine.inc) for calls of <= QUAD_MAX_DRAWS draws
+  bool quad_pref = true;       // PHY_QUAD=0: off
+  bool quad_ok = false;        // its LDS plan fits
+  size_t quad_lds = 0;
+  int* d_qprog = nullptr;      // unpacked program, nothing rebuilt (every moved partial stored)
+  double* d_qscr = nullptr;    // [wg][nslots][C][64]
+  long qscr_wgs = 0;
   bool qfuse_pref = true;      // Q-parameter chain rule inside the sweep (PHY_QFUSE=0: off)
   int cap_m = 0, nchunks = 0;  // current LDS plan
   int deep_pref = 0;           // deep stack: 0 automatic, 1 LDS, 2 global
@@ -1949,7 +1958,7 @@ void free_ctx(phy_ctx* c) {
   (void)hipSetDevice(c->device);
   void* ptrs[] = {c->d_tips,  c->d_w,     c->d_prog,    c->d_gpos,    c->d_mat_branch, c->d_pmat,
                   c->d_eig,   c->d_inner, c->d_model,   c->d_blens,   c->d_out,        c->d_site,
-                  c->d_scratch, c->d_dstk, c->d_gslot,  c->d_sslot, c->d_grows, c->d_in};
+                  c->d_scratch, c->d_dstk, c->d_gslot,  c->d_sslot, c->d_grows, c->d_in, c->d_qprog, c->d_qscr};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   if (c->h_in) (void)hipHostFree(c->h_in);
@@ -2620,10 +2629,73 @@ int launch_graphed(phy_ctx* ctx, int n, const void* bl, const void* md, const vo
   return PHY_OK;
 }
 
+// The quad sweep (quad_engine.inc) for a small call: one workgroup of C
+// waves per 16-column block and draw, as many blocks per workgroup as keep
+// the launch within one wave per SIMD; then the pattern sweep's epilogue
+// (slot sums, finalize, chain rule).
+int launch_quad(phy_ctx* ctx, int n, const double* d_blens, const double* d_model, double* d_out, double* d_site,
+                hipStream_t st, double* grows, long long gstride, bool* qdone) {
+  const int C = ctx->C, B = ctx->B;
+  const int nb = (ctx->P + QCOLS - 1) / QCOLS;
+  const int gx = std::max(1, std::min(nb, (4 * ctx->cu_count) / (C * n)));
+  const long wgs = (long)gx * n;
+  if (wgs > ctx->wg_cap || wgs > ctx->qscr_wgs) {  // grown once per context (the sampler's call size)
+    HIP_TRY(hipDeviceSynchronize());
+    if (wgs > ctx->wg_cap) {
+      int rc = alloc_wg_buffers(ctx, wgs);
+      if (rc) return rc;
+      ctx->wg_cap = (int)wgs;
+    }
+    if (wgs > ctx->qscr_wgs) {
+      if (ctx->d_qscr) (void)hipFree(ctx->d_qscr);
+      ctx->d_qscr = nullptr;
+      ctx->qscr_wgs = 0;
+      int rc = dalloc(&ctx->d_qscr, (size_t)wgs * std::max(ctx->nslots, 1) * C * WAVE);
+      if (rc) return rc;
+      ctx->qscr_wgs = wgs;
+    }
+    ++ctx->plan_gen;
+  }
+  QuadArgs qa;
+  qa.s = SweepArgs{ctx->d_tips,  ctx->d_w,     ctx->d_pmat,  d_model,      ctx->d_scratch, ctx->d_dstk,
+                   ctx->d_gslot, ctx->d_sslot, d_site,       d_out,        ctx->d_mat_branch, ctx->eig_cur,
+                   ctx->d_inner, ctx->S,       ctx->P,       ctx->Ppad,    C,              ctx->nsteps,
+                   ctx->nslots,  ctx->ndeep,   0,            ctx->nblk,    ctx->nmat,    ctx->R,         ctx->nmat,
+                   B,            phy_output_len(ctx), 0, ctx->extra, 0, d_blens, grows, gstride, 0, ctx->kind};
+  qa.qscr = ctx->d_qscr;
+  qa.nblk = nb;
+  hipEvent_t e0 = nullptr, e1 = nullptr;
+  if (ctx->timing) {
+    int rc = timing_begin(ctx, st, &e0, &e1);
+    if (rc) return rc;
+  }
+  {
+    const int* prog = ctx->d_qprog;
+    void* kargs[] = {(void*)&qa, (void*)&prog};
+    HIP_TRY(hipLaunchKernel((const void*)qsweep_kernel, dim3(gx, n), dim3(C * WAVE), kargs, ctx->quad_lds, st));
+  }
+  HIP_TRY(hipGetLastError());
+  if (ctx->timing) HIP_TRY(hipEventRecord(e1, st));
+  const int gsum_in = gx <= 16 ? 1 : 0;
+  FinArgs fa{ctx->d_gslot, ctx->d_sslot, ctx->d_pmat, ctx->eig_cur, d_blens, d_model, ctx->d_gpos, ctx->d_inner, d_out,
+             C,            B,            ctx->nmat,   gx,          phy_output_len(ctx), 0, ctx->R, grows, gstride,
+             ctx->kind,    gsum_in,      ctx->qfuse_pref ? 1 : 0};
+  if (!gsum_in) {
+    hipLaunchKernelGGL(gsum_kernel, dim3((C * B * 16 + 63) / 64, n), dim3(256), 0, st, fa);
+    HIP_TRY(hipGetLastError());
+  }
+  *qdone = launch_finalize(fa, n, st);
+  HIP_TRY(hipGetLastError());
+  return PHY_OK;
+}
+
 // The pattern sweep (sweep_kernel) and its dL/dP sums / finalize.
 int launch_pattern(phy_ctx* ctx, int n, const double* d_blens, const double* d_model, double* d_out,
                    double* d_site, hipStream_t st, double* grows, long long gstride, bool* qdone) {
   const int C = ctx->C, B = ctx->B;
+  // (an explicit column plan, phy_set_tuning(cols > 0), keeps the one / two column sweeps)
+  if (ctx->quad_ok && ctx->quad_pref && ctx->cols_pref == 0 && n <= QUAD_MAX_DRAWS && qdone)
+    return launch_quad(ctx, n, d_blens, d_model, d_out, d_site, st, grows, gstride, qdone);
   // persistent workgroups: the explicit budget, else exactly what is resident
   const int budget = ctx->wg_budget > 0 ? ctx->wg_budget : ctx->wg_resident;
   const int gx = std::max(1, std::min(ctx->nblk, (budget + n - 1) / n));
@@ -2815,6 +2887,8 @@ int phy_create(int S, int P, int C, int rooted, int model, const uint8_t* tipcod
     c->graph_pref = gk ? atoi(gk) != 0 : false;
     const char* lk = getenv("PHY_KLAT");
     c->klat_pref = lk ? atoi(lk) != 0 : true;
+    const char* qk2 = getenv("PHY_QUAD");
+    c->quad_pref = qk2 ? atoi(qk2) != 0 : true;
 
   }
   hipError_t he = hipSetDevice(device);
@@ -2839,6 +2913,7 @@ int phy_create(int S, int P, int C, int rooted, int model, const uint8_t* tipcod
     (void)hipFuncSetAttribute((const void*)res_fwd_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)LDS_CAP);
     (void)hipFuncSetAttribute((const void*)res_rev_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)LDS_CAP);
     (void)hipFuncSetAttribute((const void*)finalize_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)LDS_CAP);
+    (void)hipFuncSetAttribute((const void*)qsweep_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)LDS_CAP);
   }
   if (((size_t)C * c->B + 16 + 1024) * sizeof(double) > LDS_CAP) {
     delete c;
@@ -2925,6 +3000,19 @@ int phy_create(int S, int P, int C, int rooted, int model, const uint8_t* tipcod
     HIP_C(hipMemcpy(c->d_gpos, gpos.data(), gpos.size() * sizeof(int), hipMemcpyHostToDevice));
   }
   TRY_C(plan_chunks(c));
+  {  // the quad sweep's program: every moved partial stored (no rebuilt cherries)
+    c->quad_lds = quad_lds_bytes(S, C, c->nmat, c->R, c->ndeep);
+    c->quad_ok = c->quad_lds <= LDS_CAP;
+    if (c->quad_ok) {
+      std::vector<int> qp = c->prog;
+      for (int s = 0; s < c->nsteps; ++s) {
+        qp[(size_t)s * STEP_INTS + ST_FLAGS] &= ~(F_NOSTORE | F_PREVREC);
+        qp[(size_t)s * STEP_INTS + ST_RD] = 0;
+      }
+      TRY_C(dalloc(&c->d_qprog, qp.size()));
+      HIP_C(hipMemcpy(c->d_qprog, qp.data(), qp.size() * sizeof(int), hipMemcpyHostToDevice));
+    }
+  }
   c->h_tips.assign(tipcodes, tipcodes + (size_t)S * P);
   c->h_w.assign(weights, weights + P);
   c->h_peel.assign(peel, peel + 3 * (S - 1));

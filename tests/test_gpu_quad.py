@@ -1,0 +1,112 @@
+"""GPU: the quad sweep (csrc/quad_engine.inc) -- the pattern engine's path
+for calls of <= 32 draws (a sampler's), a quad of lanes per (pattern,
+category) column -- against the oracle and against the one / two column
+sweeps (PHY_QUAD=0), through the C-ABI.
+
+Tolerances as tests/test_gpu_parity.py: log L rel 1e-10, every gradient rel
+1e-9 of its array's largest entry.
+"""
+import numpy as np
+import pytest
+import torch  # noqa: F401 -- torch's own HIP runtime must load before the engine's
+
+from tests import cases
+from tests.test_gpu_parity import RTOL_G, RTOL_LL, _close, check_case
+
+pytestmark = pytest.mark.gpu
+
+
+def _engine(case, max_draws=1, quad=True, monkeypatch=None):
+    from phylostan_amd.engine import TreeLikelihood
+    monkeypatch.setenv("PHY_QUAD", "1" if quad else "0")
+    return TreeLikelihood(case.tipcodes, case.weights, case.peel0, case.rooted, case.model, case.C,
+                          max_draws=max_draws)
+
+
+def _draws(case, n, seed):
+    rng = np.random.default_rng(seed)
+    bl = case.blens[None, :] * rng.uniform(0.7, 1.4, (n, case.blens.size))
+    mv = np.repeat(case.model_vec()[None], n, axis=0)
+    return bl, mv
+
+
+CASES = {
+    "fluA": cases.fluA_case,
+    "HCV": cases.hcv_case,
+    "DS1": cases.ds1_case,
+    "rand_C1_JC": lambda: cases.random_case(301, S=17, P=333, C=1, model="JC69"),
+    "rand_C3_GTR": lambda: cases.random_case(302, S=40, P=500, C=3, model="GTR"),
+    "rand_C16_HKY": lambda: cases.random_case(303, S=12, P=77, C=16, model="HKY"),
+    "unrooted_C5": lambda: cases.random_case(304, S=33, P=250, C=5, model="GTR", rooted=False),
+    "caterpillar": lambda: cases.random_case(305, S=60, P=150, C=4, model="HKY", caterpillar=True),
+    "P1": lambda: cases.random_case(306, S=9, P=1, C=2, model="GTR"),
+    "all_ambiguous": lambda: cases.random_case(307, S=10, P=90, C=2, model="GTR", ambiguous=1.0),
+}
+
+
+@pytest.mark.parametrize("name", sorted(CASES))
+def test_quad_single_eval_vs_oracle(name, monkeypatch):
+    case = CASES[name]()
+    eng = _engine(case, monkeypatch=monkeypatch)
+    check_case(case, eng)
+
+
+@pytest.mark.parametrize("name", ["fluA", "HCV", "DS1", "rand_C3_GTR", "unrooted_C5", "rand_C16_HKY"])
+@pytest.mark.parametrize("n", [4, 32])
+def test_quad_batch_rows_equal_column_sweeps(name, n, monkeypatch):
+    """The sampler's shape (host buffers, n draws per call, full rows):
+    every row of the quad sweep against the one/two-column sweeps' row."""
+    case = CASES[name]()
+    bl, mv = _draws(case, n, 11)
+    quad = _engine(case, max_draws=n, monkeypatch=monkeypatch).evaluate_rows(bl, mv)
+    ref = _engine(case, max_draws=n, quad=False, monkeypatch=monkeypatch).evaluate_rows(bl, mv)
+    for k in range(n):
+        assert abs(quad[k, 0] - ref[k, 0]) <= RTOL_LL * abs(ref[k, 0]), k
+        _close(quad[k, 1:], ref[k, 1:], RTOL_G, "%s row %d" % (name, k))
+
+
+def test_quad_rows_vs_oracle_and_deterministic(monkeypatch):
+    case = cases.fluA_case()
+    n = 8
+    bl, mv = _draws(case, n, 5)
+    eng = _engine(case, max_draws=n, monkeypatch=monkeypatch)
+    a = eng.evaluate_rows(bl, mv)
+    b = eng.evaluate_rows(bl, mv)
+    assert np.array_equal(a, b), "quad sweep rows are not bitwise reproducible"
+    for k in (0, 3, 7):
+        c = cases.Case(case.name, case.tipcodes, case.weights, case.peel0, case.rooted, case.model, case.C, bl[k],
+                       case.freqs, case.rates, case.rs, case.ps)
+        ref = c.oracle()
+        assert abs(a[k, 0] - ref["loglik"]) <= RTOL_LL * abs(ref["loglik"])
+        _close(a[k, 1:1 + eng.B], ref["grad_blens"], RTOL_G, "grad_blens draw %d" % k)
+
+
+def test_quad_compact_rows_and_async_pair(monkeypatch):
+    case = cases.hcv_case()
+    n = 4
+    bl, mv = _draws(case, n, 9)
+    eng = _engine(case, max_draws=n, monkeypatch=monkeypatch)
+    eng.set_output(compact=True)
+    ref = _engine(case, max_draws=n, quad=False, monkeypatch=monkeypatch)
+    ref.set_output(compact=True)
+    r = ref.evaluate_rows(bl, mv)
+    eng.submit_rows(bl, mv)
+    q = eng.wait_rows()
+    for k in range(n):
+        assert abs(q[k, 0] - r[k, 0]) <= RTOL_LL * abs(r[k, 0])
+        _close(q[k, 1:], r[k, 1:], RTOL_G, "compact row %d" % k)
+
+
+def test_quad_impossible_draw_is_minus_inf(monkeypatch):
+    """L = 0 for one draw of a batch (a saturated branch between two
+    incompatible tips): that row is -inf, its neighbours are untouched."""
+    case = cases.random_case(310, S=6, P=40, C=2, model="JC69", ambiguous=0.0)
+    n = 3
+    bl, mv = _draws(case, n, 3)
+    eng = _engine(case, max_draws=n, monkeypatch=monkeypatch)
+    good = eng.evaluate_rows(bl, mv)
+    bl2 = bl.copy()
+    bl2[1] = 0.0  # every branch zero: P = I, tips disagree somewhere -> L = 0
+    rows = eng.evaluate_rows(bl2, mv)
+    assert rows[1, 0] == -np.inf
+    assert np.array_equal(rows[0], good[0]) and np.array_equal(rows[2], good[2])
