@@ -182,6 +182,12 @@ def survey_bytes(S, P, C, draws):
     return P * (224 * C * (S - 2) + 3 * S + 16) * draws
 
 
+def survey_flops(S, P, C, draws):
+    """SURVEY.md 8d's algorithmic flops: F_eval = 244 C P (S-1) (forward 60
+    per node, reverse 92 per branch)."""
+    return 244.0 * C * P * (S - 1) * draws
+
+
 def host_cpu_info():
     """CPU model, nproc, and the host threads this job may use: the CPUs in
     its affinity mask, capped by a cgroup CPU quota when one is set (the GPU
@@ -626,6 +632,15 @@ def main():
                 "kernel": kernel_name, "kernel_avg_ms": kern_avg_ms,
                 "algorithmic_bytes_per_launch": alg,
                 "survey_model_bytes_per_launch": survey_bytes(S, P_local, C, draws),
+                # SURVEY.md 8d's flops per evaluation over the same launch time, against the fp64 vector peak
+                "survey_flops_frac": survey_flops(S, P_local, C, draws) / (kern_avg_ms * 1e-3) / 1e12
+                / PEAK_FP64_TFLOPS,
+                # what actually limits the kernel: the byte roof above is the bound the
+                # contract prices against; the counters say instruction issue / latency
+                "limiter": ("issue/latency: SQ counters show the SIMDs issuing about half of the wave-cycles "
+                            "and waiting on s_waitcnt most of the rest (profiles/sq_counters.json); counted HBM "
+                            "traffic is below the 8 TB/s roof" if info["engine"] == "pattern" else
+                            "latency / launch chain: one small dependent kernel per tree level (DESIGN.md 5b)"),
                 "compute": compute,
             },
             "cpu_baseline": cpu,

@@ -1683,10 +1683,19 @@ struct FusedG {
       const double* src = a.gslot + (size_t)draw * a.gx * per_wg + ((size_t)c * a.nmat + mm) * 16 + k * 4;
       double2 lo = *reinterpret_cast<const double2*>(src), hi = *reinterpret_cast<const double2*>(src + 2);
       r[0] = lo.x; r[1] = lo.y; r[2] = hi.x; r[3] = hi.y;
-      for (int w = 1; w < a.gx; ++w) {
-        lo = *reinterpret_cast<const double2*>(src + (size_t)w * per_wg);
-        hi = *reinterpret_cast<const double2*>(src + (size_t)w * per_wg + 2);
-        r[0] += lo.x; r[1] += lo.y; r[2] += hi.x; r[3] += hi.y;
+      for (int w0 = 1; w0 < a.gx; w0 += 8) {  // 8 slots in flight, summed in slot order
+        double2 l8[8], h8[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          const int w = w0 + u < a.gx ? w0 + u : 0;
+          l8[u] = *reinterpret_cast<const double2*>(src + (size_t)w * per_wg);
+          h8[u] = *reinterpret_cast<const double2*>(src + (size_t)w * per_wg + 2);
+        }
+#pragma unroll
+        for (int u = 0; u < 8; ++u)
+          if (w0 + u < a.gx) {
+            r[0] += l8[u].x; r[1] += l8[u].y; r[2] += h8[u].x; r[3] += h8[u].y;
+          }
       }
       *reinterpret_cast<double2*>(grow) = make_double2(r[0], r[1]);
       *reinterpret_cast<double2*>(grow + 2) = make_double2(r[2], r[3]);
@@ -1738,7 +1747,14 @@ __global__ void __launch_bounds__(1024) finalize_kernel(FinArgs a) {
       const int b = rem >> 4, k = rem & 15;
       const double* src = base + ((size_t)c * a.nmat + a.gpos[b]) * 16 + k;
       double s = src[0];
-      for (int w = 1; w < a.gx; ++w) s += src[(size_t)w * per_wg];
+      for (int w0 = 1; w0 < a.gx; w0 += 8) {  // 8 slots in flight, summed in slot order
+        double v8[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) v8[u] = src[(size_t)(w0 + u < a.gx ? w0 + u : 0) * per_wg];
+#pragma unroll
+        for (int u = 0; u < 8; ++u)
+          if (w0 + u < a.gx) s += v8[u];
+      }
       a.grows[(size_t)draw * a.grows_stride + idx] = s;
     }
   }
@@ -2431,11 +2447,9 @@ int launch_class(phy_ctx* ctx, int n, const double* d_blens, const double* d_mod
       a.count = L.ntile;
       hipLaunchKernelGGL(cls_red_kernel, dim3((L.ntile + 3) / 4, dcn), dim3(256), 0, st, a);
     }
-    if (L.nspan && !e->tickets) {
-      a.first = L.span0;
-      a.count = L.nspan;
-      hipLaunchKernelGGL(cls_fix_kernel, dim3((L.nspan + 3) / 4, dcn), dim3(256), 0, st, a);
-    }
+    if (L.nlfix)  // the level's long spans (the short ones are summed by the REV lanes)
+      hipLaunchKernelGGL(cls_fix_list_kernel, dim3((L.nlfix + 3) / 4, dcn), dim3(256), 0, st, a,
+                         (const int*)e->d_lfix + L.lfix0, L.nlfix);
     if (L.nchunk) {
       a.first = L.chunk0;
       a.count = L.nchunk;
@@ -2446,7 +2460,7 @@ int launch_class(phy_ctx* ctx, int n, const double* d_blens, const double* d_mod
     if (e->nrtile)
       hipLaunchKernelGGL(cls_red_list_kernel, dim3((e->nrtile + 3) / 4, dcn), dim3(256), 0, st, a,
                          (const int*)e->d_rtile, e->nrtile);
-    if (e->nrspan && !e->tickets)
+    if (e->nrspan)
       hipLaunchKernelGGL(cls_fix_list_kernel, dim3((e->nrspan + 3) / 4, dcn), dim3(256), 0, st, a,
                          (const int*)e->d_rspan, e->nrspan);
     hipLaunchKernelGGL(cls_clade_rev_kernel, dim3(e->nclade, dcn), dim3(CLADE_THREADS), 0, st, a,
