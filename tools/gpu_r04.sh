@@ -47,15 +47,6 @@ if want multidev; then
     --no-cpu-baseline --json-out $O/bench_multidev1.json > $O/bench_multidev1.log 2>&1
   python -c "import json;d=json.load(open('$O/bench_multidev1.json'));print('multidev1', d['value'], d['config']['parallelism'])"
 fi
-if want ticketab; then  # class sweep: FIX launches (default) against ticketed spans, alternating
-  for rep in 1 2; do
-    for tk in 0 1; do
-      PHY_TICKETS=$tk timeout -k 10 200 python bench.py --workload synthetic --shard-of 8 --steps 100 --warmup 10 \
-        --no-cpu-baseline --json-out $O/shard8_tk${tk}_$rep.json > $O/shard8_tk${tk}_$rep.log 2>&1
-      python -c "import json;d=json.load(open('$O/shard8_tk${tk}_$rep.json'));print('shard8 tickets=$tk', d['value'], d['ms_per_step'])"
-    done
-  done
-fi
 if want prof; then
   timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof_fluA -o run -- \
     python bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-sampler-latency > $O/prof_fluA.log 2>&1
