@@ -498,18 +498,18 @@ struct QgArgs {
 constexpr int QG_THREADS = 1024;  // 256 (c, b) quads per pass (the synthetic config: 1016 in 4 passes, not 16)
 constexpr int QG_SHARED = 16 * 3 + 4 + (QG_THREADS / 64) * 16 + 16 * 2;  // V, V^-1, 1/(lam_k - lam_l), lam,
                                                                           // wave partials, M, W
-// The (c, b) item's dL/dP block G (row-major 4x4) for qgrad_body: by default
-// the draw's dL/dP row (every lane of the item's quad loads all 16).
+// Row k of the (c, b) item's dL/dP block G (row-major 4x4) for lane k of the
+// item's quad in qgrad_body (the other rows come by quad broadcast): by
+// default from the draw's dL/dP row.
 struct RowsG {
   const double* rows;
-  __device__ __forceinline__ void operator()(int idx, int, double (&G)[16]) const {
-    const double2* g2 = reinterpret_cast<const double2*>(rows + (size_t)idx * 16);
-#pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      const double2 v = g2[u];
-      G[2 * u] = v.x;
-      G[2 * u + 1] = v.y;
-    }
+  __device__ __forceinline__ void operator()(int idx, int k, double (&g)[4]) const {
+    const double2* g2 = reinterpret_cast<const double2*>(rows + (size_t)idx * 16 + k * 4);
+    const double2 lo = g2[0], hi = g2[1];
+    g[0] = lo.x;
+    g[1] = lo.y;
+    g[2] = hi.x;
+    g[3] = hi.y;
   }
 };
 template <typename GP>
@@ -557,8 +557,8 @@ __device__ void qgrad_body(const QgArgs& a, int draw, int tid, double* sh, const
     for (int idx = vt >> 2; idx < C * B; idx += QG_THREADS / 4) {
       const int c = idx / B, b = idx - c * B;
       const double t = mdl[10 + c] * bl[b];
-      double G[16];
-      getG(idx, k, G);
+      double g[4];  // row k of G; G[i][j] = row i's g[j], broadcast from lane i of the quad
+      getG(idx, k, g);
       const double Ek = exp(slam[k] * t);
       double E[4];
       E[0] = dpp_d<0x00>(Ek);
@@ -568,10 +568,8 @@ __device__ void qgrad_body(const QgArgs& a, int draw, int tid, double* sh, const
       double T[4];  // row k of V^T G
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
-        double acc = 0.0;
-#pragma unroll
-        for (int i = 0; i < 4; ++i) acc = fma(sV[i * 4 + k], G[i * 4 + j], acc);
-        T[j] = acc;
+        const double g0 = dpp_d<0x00>(g[j]), g1 = dpp_d<0x55>(g[j]), g2 = dpp_d<0xAA>(g[j]), g3 = dpp_d<0xFF>(g[j]);
+        T[j] = fma(sV[12 + k], g3, fma(sV[8 + k], g2, fma(sV[4 + k], g1, fma(sV[k], g0, 0.0))));
       }
 #pragma unroll
       for (int l = 0; l < 4; ++l) {
@@ -1664,7 +1662,7 @@ __global__ void __launch_bounds__(256) gsum_kernel(FinArgs a) {
 // The fused epilogue's dL/dP provider (finalize_kernel with the chain rule):
 // lane k of the (c, b) item's quad forms row k of G -- the sum of the gx
 // workgroup slots (gsum_in; written out as the dL/dP row) or the row
-// itself -- then the quad shares its rows by DPP, and its share of <G, Q P>
+// itself -- qgrad_body broadcasts the rows inside the quad, and its share of <G, Q P>
 // goes to inner[idx] after a quad sum.  One pass over the items instead of
 // slot sums -> HBM -> <G, QP> -> HBM -> the chain rule's reads.
 struct FusedG {
@@ -1672,7 +1670,7 @@ struct FusedG {
   int draw;
   double* inner;    // LDS [C*B]
   const double* Q;  // LDS [16]
-  __device__ __forceinline__ void operator()(int idx, int k, double (&G)[16]) const {
+  __device__ __forceinline__ void operator()(int idx, int k, double (&g)[4]) const {
     const int C = a.C, B = a.B;
     const int c = idx / B, b = idx - c * B;
     const int mm = a.gpos[b];
@@ -1683,16 +1681,16 @@ struct FusedG {
       const double* src = a.gslot + (size_t)draw * a.gx * per_wg + ((size_t)c * a.nmat + mm) * 16 + k * 4;
       double2 lo = *reinterpret_cast<const double2*>(src), hi = *reinterpret_cast<const double2*>(src + 2);
       r[0] = lo.x; r[1] = lo.y; r[2] = hi.x; r[3] = hi.y;
-      for (int w0 = 1; w0 < a.gx; w0 += 8) {  // 8 slots in flight, summed in slot order
-        double2 l8[8], h8[8];
+      for (int w0 = 1; w0 < a.gx; w0 += 4) {  // 4 slots (8 loads) in flight, summed in slot order
+        double2 l8[4], h8[4];  // (8 slots spill at 1,024 threads)
 #pragma unroll
-        for (int u = 0; u < 8; ++u) {
+        for (int u = 0; u < 4; ++u) {
           const int w = w0 + u < a.gx ? w0 + u : 0;
           l8[u] = *reinterpret_cast<const double2*>(src + (size_t)w * per_wg);
           h8[u] = *reinterpret_cast<const double2*>(src + (size_t)w * per_wg + 2);
         }
 #pragma unroll
-        for (int u = 0; u < 8; ++u)
+        for (int u = 0; u < 4; ++u)
           if (w0 + u < a.gx) {
             r[0] += l8[u].x; r[1] += l8[u].y; r[2] += h8[u].x; r[3] += h8[u].y;
           }
@@ -1704,12 +1702,7 @@ struct FusedG {
       r[0] = lo.x; r[1] = lo.y; r[2] = hi.x; r[3] = hi.y;
     }
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      G[j] = dpp_d<0x00>(r[j]);
-      G[4 + j] = dpp_d<0x55>(r[j]);
-      G[8 + j] = dpp_d<0xAA>(r[j]);
-      G[12 + j] = dpp_d<0xFF>(r[j]);
-    }
+    for (int j = 0; j < 4; ++j) g[j] = r[j];
     // row k of <G, Q P>: sum_j G[k][j] (Q P)[k][j]; P column-major in its record
     const double* P = a.pmat + ((size_t)draw * C * a.nmat + (size_t)c * a.nmat + mm) * a.R * 4;
     double sv = 0.0;

@@ -1,5 +1,5 @@
 """GPU: the quad sweep (csrc/quad_engine.inc) -- the pattern engine's path
-for calls of <= 32 draws (a sampler's), a quad of lanes per (pattern,
+for calls of <= 16 draws (a sampler's), a quad of lanes per (pattern,
 category) column -- against the oracle and against the one / two column
 sweeps (PHY_QUAD=0), through the C-ABI.
 
@@ -52,7 +52,7 @@ def test_quad_single_eval_vs_oracle(name, monkeypatch):
 
 
 @pytest.mark.parametrize("name", ["fluA", "HCV", "DS1", "rand_C3_GTR", "unrooted_C5", "rand_C16_HKY"])
-@pytest.mark.parametrize("n", [4, 32])
+@pytest.mark.parametrize("n", [4, 16])
 def test_quad_batch_rows_equal_column_sweeps(name, n, monkeypatch):
     """The sampler's shape (host buffers, n draws per call, full rows):
     every row of the quad sweep against the one/two-column sweeps' row."""

@@ -65,4 +65,22 @@ if want lat; then  # small calls: quad sweep against the column sweeps (PHY_QUAD
   timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof_lat4 -o run -- \
     python tools/latency_probe.py --workload fluA --draws 4 --engine pattern > $O/prof_lat4.log 2>&1
 fi
+if want lat4; then  # the sampler's call only (4 draws), every engine, plus its kernel trace
+  for w in fluA HCV DS1; do
+    for q in 1 0; do
+      PHY_QUAD=$q timeout -k 10 120 python tools/latency_probe.py --workload $w --draws 4 --engine pattern \
+        > $O/lat4_${w}_q$q.log 2>&1 && tail -1 $O/lat4_${w}_q$q.log | sed "s/^/$w d=4 quad=$q /"
+    done
+  done
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof_lat4 -o run -- \
+    python tools/latency_probe.py --workload fluA --draws 4 --engine pattern > $O/prof_lat4.log 2>&1
+  python tools/prof_stats.py $O/prof_lat4/run_results.db
+fi
+if want sq4; then  # SQ counters of the quad sweep on the 4-draw fluA call (separate --pmc passes)
+  PMC_SCRIPT=tools/latency_probe.py PMC_KERNEL=qsweep timeout -k 10 600 python tools/pmc_sq.py \
+    --workload fluA --draws 4 --engine pattern --calls 50 > $O/sq4_qsweep.json 2> $O/sq4_qsweep.err
+  PMC_SCRIPT=tools/latency_probe.py PMC_KERNEL=finalize timeout -k 10 600 python tools/pmc_sq.py \
+    --workload fluA --draws 4 --engine pattern --calls 50 > $O/sq4_finalize.json 2> $O/sq4_finalize.err
+  head -c 600 $O/sq4_qsweep.json
+fi
 echo done

@@ -1,7 +1,9 @@
 #!/usr/bin/env python
 """Collect SQ / TCC counters of the sweep kernel in separate rocprofv3 --pmc
 passes (kernel-trace only) and print per-dispatch averages.  Run on the GPU
-box:  python tools/pmc_sq.py [bench.py args ...]"""
+box:  python tools/pmc_sq.py [bench.py args ...]
+PMC_KERNEL=name: that kernel's dispatches only; PMC_SCRIPT=tools/latency_probe.py:
+profile that script (with the given args) instead of bench.py."""
 import csv
 import glob
 import json
@@ -25,7 +27,8 @@ def main():
         d = os.path.join(ROOT, "gpurun_out", "pmc_sq", "p%d" % k)
         cmd = ["rocprofv3", "--kernel-trace", "-d", d, "-o", "run", "--output-format", "csv"]
         cmd += ["--pmc"] + counters.split()
-        cmd += ["--", sys.executable, os.path.join(ROOT, "bench.py")] + bench_args
+        script = os.environ.get("PMC_SCRIPT", "bench.py")
+        cmd += ["--", sys.executable, os.path.join(ROOT, script)] + bench_args
         r = subprocess.run(cmd, stdout=subprocess.DEVNULL, stderr=subprocess.PIPE, timeout=180,
                            env=dict(os.environ, TMPDIR="/tmp"))
         if r.returncode != 0:
@@ -56,7 +59,7 @@ def main():
             out[cn] = v / max(nev.get(cn, 1), 1)
     print(json.dumps(out, indent=1))
     # keyed record for bench.py's roofline.compute (same kernel source only)
-    if not os.environ.get("PMC_KERNEL") and "SQ_INSTS_VALU_FMA_F64" in out and "SQ_WAVE_CYCLES" in out:
+    if not os.environ.get("PMC_KERNEL") and not os.environ.get("PMC_SCRIPT") and "SQ_INSTS_VALU_FMA_F64" in out and "SQ_WAVE_CYCLES" in out:
         sys.path.insert(0, ROOT)
         from bench import kernel_source_hash
         wl = bench_args[bench_args.index("--workload") + 1] if "--workload" in bench_args else "fluA"
