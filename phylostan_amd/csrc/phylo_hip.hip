@@ -512,6 +512,54 @@ struct RowsG {
     g[3] = hi.y;
   }
 };
+// The Q-parameter tail every epilogue ends with (one thread): from
+// W = V^-T M V^T the exchangeability gradients oq[4..9] and the frequency
+// gradients oq[10..13] (plus the root-frequency term rt[0..3]) through
+// Q = S^-1 R diag(f) with S the normaliser (generate_script.py's GTR / HKY
+// rate matrix; models.q_param_gradients is the host statement).
+__device__ void q_tail(const double (&W)[16], const double* Q, double sn, const double* mdl, const double* rt,
+                       double* oq) {
+  double qw = 0.0;
+#pragma unroll
+  for (int kk = 0; kk < 16; ++kk) qw = fma(Q[kk], W[kk], qw);
+  const double f[4] = {mdl[0], mdl[1], mdl[2], mdl[3]};
+  const double* r = mdl + 4;  // AC AG AT CG CT GT
+  const int pi_[6] = {0, 0, 0, 1, 1, 2}, pj_[6] = {1, 2, 3, 2, 3, 3};
+  double Rm[16];
+#pragma unroll
+  for (int kk = 0; kk < 16; ++kk) Rm[kk] = 0.0;
+#pragma unroll
+  for (int kk = 0; kk < 6; ++kk) {
+    const int i = pi_[kk], j = pj_[kk];
+    Rm[i * 4 + j] = Rm[j * 4 + i] = r[kk];
+    const double dq = f[j] * W[i * 4 + j] + f[i] * W[j * 4 + i] - f[j] * W[i * 4 + i] - f[i] * W[j * 4 + j];
+    oq[4 + kk] = (dq - 2.0 * f[i] * f[j] * qw) / sn;
+  }
+#pragma unroll
+  for (int mm = 0; mm < 4; ++mm) {
+    double dq = 0.0, ds = 0.0;
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      if (j != mm) {
+        dq += Rm[j * 4 + mm] * (W[j * 4 + mm] - W[j * 4 + j]);
+        ds += 2.0 * Rm[mm * 4 + j] * f[j];
+      }
+    oq[10 + mm] = (dq - ds * qw) / sn + rt[mm];
+  }
+}
+
+// W = V^-T M V^T, entry t = (i, j) (every epilogue's order)
+__device__ __forceinline__ double w_entry(const double* M, const double* V, const double* Vi, int t) {
+  const int i = t >> 2, j = t & 3;
+  double acc = 0.0;
+  for (int kk = 0; kk < 4; ++kk) {
+    double ml = 0.0;
+    for (int l = 0; l < 4; ++l) ml = fma(M[kk * 4 + l], V[j * 4 + l], ml);
+    acc = fma(Vi[kk * 4 + i], ml, acc);
+  }
+  return acc;
+}
+
 template <typename GP>
 __device__ void qgrad_body(const QgArgs& a, int draw, int tid, double* sh, const GP& getG);
 __device__ __forceinline__ void qgrad_body(const QgArgs& a, int draw, int tid, double* sh) {
@@ -603,49 +651,12 @@ __device__ void qgrad_body(const QgArgs& a, int draw, int tid, double* sh, const
     sM[tid] = acc;
   }
   __syncthreads();
-  if (tid < 16) {
-    const int i = tid >> 2, j = tid & 3;
-    double acc = 0.0;
-    for (int kk = 0; kk < 4; ++kk) {
-      double ml = 0.0;
-      for (int l = 0; l < 4; ++l) ml = fma(sM[kk * 4 + l], sV[j * 4 + l], ml);
-      acc = fma(sVi[kk * 4 + i], ml, acc);
-    }
-    sW[tid] = acc;
-  }
+  if (tid < 16) sW[tid] = w_entry(sM, sV, sVi, tid);
   __syncthreads();
   if (tid != 0) return;
   double W[16];
   for (int kk = 0; kk < 16; ++kk) W[kk] = sW[kk];
-  const double* Q = e + EIG_Q;
-  const double sn = e[EIG_S];
-  double qw = 0.0;
-#pragma unroll
-  for (int kk = 0; kk < 16; ++kk) qw = fma(Q[kk], W[kk], qw);
-  const double f[4] = {mdl[0], mdl[1], mdl[2], mdl[3]};
-  const double* r = mdl + 4;  // AC AG AT CG CT GT
-  const int pi_[6] = {0, 0, 0, 1, 1, 2}, pj_[6] = {1, 2, 3, 2, 3, 3};
-  double Rm[16];
-#pragma unroll
-  for (int kk = 0; kk < 16; ++kk) Rm[kk] = 0.0;
-#pragma unroll
-  for (int kk = 0; kk < 6; ++kk) {
-    const int i = pi_[kk], j = pj_[kk];
-    Rm[i * 4 + j] = Rm[j * 4 + i] = r[kk];
-    const double dq = f[j] * W[i * 4 + j] + f[i] * W[j * 4 + i] - f[j] * W[i * 4 + i] - f[i] * W[j * 4 + j];
-    out[o + 4 + kk] = (dq - 2.0 * f[i] * f[j] * qw) / sn;
-  }
-#pragma unroll
-  for (int mm = 0; mm < 4; ++mm) {
-    double dq = 0.0, ds = 0.0;
-#pragma unroll
-    for (int j = 0; j < 4; ++j)
-      if (j != mm) {
-        dq += Rm[j * 4 + mm] * (W[j * 4 + mm] - W[j * 4 + j]);
-        ds += 2.0 * Rm[mm * 4 + j] * f[j];
-      }
-    out[o + 10 + mm] = (dq - ds * qw) / sn + out[o + mm];
-  }
+  q_tail(W, e + EIG_Q, e[EIG_S], mdl, out + o, out + o);
 }
 
 // The sweep.  `prog` is a separate __restrict__ const argument so the
@@ -1858,6 +1869,238 @@ __global__ void __launch_bounds__(QG_THREADS) qgrad_kernel(FinArgs a) {
   qgrad_body(q, blockIdx.x, threadIdx.x, sh);
 }
 
+// The small call's epilogue split over workgroups (the quad sweep's, <= 16
+// draws of <= 16 workgroup slots each).  One 1,024-thread workgroup per draw
+// (finalize_kernel) reads the draw's ~1 MB of slots (fluA: 15 x C x nmat x
+// 16 doubles, written by workgroups on other XCDs: L2 misses) through ONE
+// CU, 16 dependent rounds: 25 us of a 125 us sampler call (r04f SQ: 67% of
+// the waves' cycles waiting).  Here workgroup s of a draw owns branches
+// [s bper, (s + 1) bper) in every category, a quad of lanes per (c, b)
+// item with every slot load of the item in flight at once:
+//   * row k of G_cb = the slots summed in slot order -> the dL/dP row;
+//   * <G_cb, Q P_cb> (finalize's order) -> dlogL/db = sum_c r_c (.) for the
+//     owned branches directly, sum_b b (.) per category as a hand-off;
+//   * the item's share of M = sum_cb (V^T G V^-T) o Phi (qgrad_body's
+//     terms), summed over the workgroup's items in a fixed tree -> hand-off;
+//   * workgroup 0 also sums the scalar slots (log L, dlogL/dps, the root
+//     frequency term).
+// Hand-offs are write-through agent-scope stores; the draw's last workgroup
+// (a ticket) takes one acquire and sums the hand-offs in workgroup order,
+// then W = V^-T M V^T and q_tail.  Deterministic: every sum has a fixed
+// order (not finalize_kernel's bits: M and sum_b b (.) are summed per
+// workgroup first).
+constexpr int QFIN_THREADS = 256;
+constexpr int QFIN_ITEMS = QFIN_THREADS / 4;  // (c, b) items per workgroup
+constexpr int QFIN_SLOTS = 16;                // workgroup slots per draw it takes
+struct QfinArgs {
+  FinArgs f;
+  double* part;              // [draw][nspl][16 + C] hand-offs: M partial, sum_b b <G, QP> per category
+  unsigned long long* cnt;   // [draw] tickets (modulo nspl; zeroed at allocation)
+  int bper, nspl;
+};
+__global__ void __launch_bounds__(QFIN_THREADS) qfin_kernel(QfinArgs qa) {
+  const FinArgs& a = qa.f;
+  __shared__ double sV[16], sVi[16], sQ[16], srinv[16], slam[4];
+  __shared__ double sinner[QFIN_ITEMS];
+  __shared__ double wpart[QFIN_THREADS / 64][16];
+  __shared__ double sred[8 * 16];
+  __shared__ double sM[16];
+  __shared__ int s_last;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int sp = blockIdx.x, draw = blockIdx.y;
+  const int C = a.C, B = a.B, bper = qa.bper, nspl = qa.nspl, gx = a.gx;
+  const int b0 = sp * bper, nb = min(bper, B - b0);
+  const bool qp = a.kind != PHY_JC69;
+  const double* eg = a.eig + (size_t)draw * EIG_LEN;
+  const double* mdl = a.model + (size_t)draw * (10 + 2 * C);
+  const double* blv = a.blens + (size_t)draw * B;
+  double* out = a.out + (size_t)draw * a.outlen;
+  const int o = 1 + B + 2 * C;
+  const int li = tid >> 2, k = tid & 3;
+  const int c = li / bper, bl = li - c * bper;
+  const bool live = c < C && bl < nb;  // quad-uniform
+  const int b = b0 + (live ? bl : 0), idx = c * B + b, mm = a.gpos[b];
+  // every global load of the item first (slots, P record), then the
+  // eigensystem's staging barrier: one memory round trip, not three
+  double2 lo[QFIN_SLOTS], hi[QFIN_SLOTS], p01[4], p23[4];
+  if (live) {
+    const size_t per_wg = (size_t)C * a.nmat * 16;
+    const double* src = a.gslot + (size_t)draw * gx * per_wg + ((size_t)c * a.nmat + mm) * 16 + k * 4;
+#pragma unroll
+    for (int w = 0; w < QFIN_SLOTS; ++w)
+      if (w < gx) {
+        lo[w] = *reinterpret_cast<const double2*>(src + (size_t)w * per_wg);
+        hi[w] = *reinterpret_cast<const double2*>(src + (size_t)w * per_wg + 2);
+      }
+    const double* P = a.pmat + ((size_t)draw * C * a.nmat + (size_t)c * a.nmat + mm) * a.R * 4;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      p01[j] = *reinterpret_cast<const double2*>(P + j * 4);
+      p23[j] = *reinterpret_cast<const double2*>(P + j * 4 + 2);
+    }
+  }
+  if (tid < 16) {
+    sV[tid] = eg[EIG_M1 + tid];
+    sVi[tid] = eg[EIG_M2 + tid];
+    sQ[tid] = eg[EIG_Q + tid];
+    const double lk = eg[EIG_LAM + (tid >> 2)], ll = eg[EIG_LAM + (tid & 3)];
+    const double d = lk - ll;
+    srinv[tid] = fabs(d) < 1e-12 * fmax(1.0, fabs(lk)) ? 0.0 : 1.0 / d;  // 0: tie (qgrad_body's rule)
+    if (tid < 4) slam[tid] = eg[EIG_LAM + tid];
+  }
+  __syncthreads();
+  double m[4] = {0.0, 0.0, 0.0, 0.0};
+  if (live) {
+    double r[4] = {lo[0].x, lo[0].y, hi[0].x, hi[0].y};
+#pragma unroll
+    for (int w = 1; w < QFIN_SLOTS; ++w)
+      if (w < gx) {
+        r[0] += lo[w].x;
+        r[1] += lo[w].y;
+        r[2] += hi[w].x;
+        r[3] += hi[w].y;
+      }
+    double* grow = a.grows + (size_t)draw * a.grows_stride + (size_t)idx * 16 + k * 4;
+    *reinterpret_cast<double2*>(grow) = make_double2(r[0], r[1]);
+    *reinterpret_cast<double2*>(grow + 2) = make_double2(r[2], r[3]);
+    // row k of <G, Q P> (FusedG's order), then the quad's sum
+    double sv = 0.0;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const double qpv = fma(sQ[k * 4 + 3], p23[j].y,
+                             fma(sQ[k * 4 + 2], p23[j].x, fma(sQ[k * 4 + 1], p01[j].y, sQ[k * 4] * p01[j].x)));
+      sv = fma(r[j], qpv, sv);
+    }
+    sv += dpp_d<0xB1>(sv);  // quad_perm [1,0,3,2]
+    sv += dpp_d<0x4E>(sv);  // quad_perm [2,3,0,1]
+    if (k == 0) sinner[li] = sv;
+    if (qp) {  // row k of this item's M term (qgrad_body's arithmetic)
+      const double t = mdl[10 + c] * blv[b];
+      const double Ek = exp(slam[k] * t);
+      double E[4];
+      E[0] = dpp_d<0x00>(Ek);
+      E[1] = dpp_d<0x55>(Ek);
+      E[2] = dpp_d<0xAA>(Ek);
+      E[3] = dpp_d<0xFF>(Ek);
+      double T[4];  // row k of V^T G
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const double g0 = dpp_d<0x00>(r[j]), g1 = dpp_d<0x55>(r[j]), g2 = dpp_d<0xAA>(r[j]), g3 = dpp_d<0xFF>(r[j]);
+        T[j] = fma(sV[12 + k], g3, fma(sV[8 + k], g2, fma(sV[4 + k], g1, fma(sV[k], g0, 0.0))));
+      }
+#pragma unroll
+      for (int l = 0; l < 4; ++l) {
+        double hh = 0.0;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) hh = fma(T[j], sVi[l * 4 + j], hh);
+        const double ri = srinv[k * 4 + l];
+        const double phi = ri == 0.0 ? t * Ek : (Ek - E[l]) * ri;
+        m[l] = hh * phi;
+      }
+    }
+  }
+  // the wave's 16 quads (qgrad_body's butterfly), then the waves in order
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    swap32(m[u], m[u + 2]);
+    m[u] += m[u + 2];
+  }
+  swap16(m[0], m[1]);
+  m[0] += m[1];
+  m[0] += dpp_d<DPP_ROW_ROR8>(m[0]);
+  m[0] += dpp_d<0x124>(m[0]);
+  if ((lane & 12) == 0) wpart[wave][k * 4 + ((lane >> 5) & 1) * 2 + ((lane >> 4) & 1)] = m[0];
+  if (sp == 0 && tid < 8 * C) {  // scalar slots, in slot order (finalize_kernel's bits)
+    const double* ss = a.sslot + (size_t)draw * gx * 8 * C + tid;
+    double acc = ss[0];
+    for (int w = 1; w < gx; ++w) acc += ss[(size_t)w * 8 * C];
+    sred[tid] = acc;
+  }
+  __syncthreads();
+  const double* rs = mdl + 10;
+  if (tid < nb) {  // dlogL/db of the owned branches (finalize's order over c)
+    double sv = 0.0;
+    for (int cc = 0; cc < C; ++cc) sv = fma(rs[cc], sinner[cc * bper + tid], sv);
+    out[1 + b0 + tid] = sv;
+  }
+  double* hp = qa.part + ((size_t)draw * nspl + sp) * (16 + C);
+  if (tid >= 64 && tid < 80) {
+    const int t = tid - 64;
+    double acc = wpart[0][t];
+    for (int w = 1; w < QFIN_THREADS / 64; ++w) acc += wpart[w][t];
+    __hip_atomic_store(hp + t, acc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  if (tid >= 128 && tid < 128 + C) {
+    const int cc = tid - 128;
+    double acc = 0.0;
+    for (int j = 0; j < nb; ++j) acc = fma(blv[b0 + j], sinner[cc * bper + j], acc);
+    __hip_atomic_store(hp + 16 + cc, acc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  if (sp == 0 && tid == 0) {
+    const double ll = sred[0];
+    out[0] = isfinite(ll) ? ll : -INFINITY;
+    for (int cc = 0; cc < C; ++cc) out[1 + B + C + cc] = sred[cc * 8 + 1];
+    for (int f = 0; f < 4; ++f) {
+      double t = 0.0;
+      for (int cc = 0; cc < C; ++cc) t += sred[cc * 8 + 2 + f];
+      __hip_atomic_store(out + o + f, t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains its write-through hand-offs
+  __syncthreads();
+  if (tid == 0) {
+    const unsigned long long old = __hip_atomic_fetch_add(qa.cnt + draw, 1ull, __ATOMIC_RELAXED,
+                                                          __HIP_MEMORY_SCOPE_AGENT);
+    s_last = ((old + 1) % (unsigned long long)nspl) == 0;
+  }
+  __syncthreads();
+  if (!s_last) return;
+  // the draw's last workgroup: every hand-off was stored sc1 and drained
+  // before its ticket, and EVERY load of one here is an sc1 load
+  // (agent-scope atomic), so no acquire fence (cdna_hip_programming.md
+  // Guideline 16, the sc1-load form); the other loads read launch inputs
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  const double* pp = qa.part + (size_t)draw * nspl * (16 + C);
+  auto ld1 = [](const double* q) { return __hip_atomic_load(q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); };
+  if (tid < 16) {
+    double u[8];  // 8 hand-offs in flight, summed in workgroup order
+    double acc = 0.0;
+    for (int q0 = 0; q0 < nspl; q0 += 8) {
+#pragma unroll
+      for (int v = 0; v < 8; ++v) u[v] = q0 + v < nspl ? ld1(pp + (size_t)(q0 + v) * (16 + C) + tid) : 0.0;
+#pragma unroll
+      for (int v = 0; v < 8; ++v)
+        if (q0 + v < nspl) acc = (q0 + v == 0) ? u[v] : acc + u[v];
+    }
+    sM[tid] = acc;
+  }
+  if (tid >= 64 && tid < 64 + C) {
+    const int cc = tid - 64;
+    double u[8];
+    double acc = 0.0;
+    for (int q0 = 0; q0 < nspl; q0 += 8) {
+#pragma unroll
+      for (int v = 0; v < 8; ++v) u[v] = q0 + v < nspl ? ld1(pp + (size_t)(q0 + v) * (16 + C) + 16 + cc) : 0.0;
+#pragma unroll
+      for (int v = 0; v < 8; ++v)
+        if (q0 + v < nspl) acc = (q0 + v == 0) ? u[v] : acc + u[v];
+    }
+    out[1 + B + cc] = acc;
+  }
+  if (!qp) {
+    if (tid < 10) out[o + 4 + tid] = 0.0;
+    return;
+  }
+  __syncthreads();
+  if (tid < 16) wpart[0][tid] = w_entry(sM, sV, sVi, tid);
+  __syncthreads();
+  if (tid != 0) return;
+  double W[16];
+  for (int t = 0; t < 16; ++t) W[t] = wpart[0][t];
+  const double rt[4] = {ld1(out + o), ld1(out + o + 1), ld1(out + o + 2), ld1(out + o + 3)};  // workgroup 0's
+  q_tail(W, sQ, eg[EIG_S], mdl, rt, out + o);
+}
+
 }  // namespace
 
 // ---------------------------------------------------------------------------
@@ -1888,6 +2131,8 @@ struct phy_ctx {
   size_t quad_lds = 0;
   int* d_qprog = nullptr;      // unpacked program, nothing rebuilt (every moved partial stored)
   double* d_qscr = nullptr;    // [wg][nslots][C][64]
+  double* d_qfpart = nullptr;  // qfin_kernel hand-offs [QUAD_MAX_DRAWS][nspl][16 + C]
+  unsigned long long* d_qfcnt = nullptr;  // its tickets [QUAD_MAX_DRAWS]
   long qscr_wgs = 0;
   bool qfuse_pref = true;      // Q-parameter chain rule inside the sweep (PHY_QFUSE=0: off)
   int cap_m = 0, nchunks = 0;  // current LDS plan
@@ -1967,7 +2212,8 @@ void free_ctx(phy_ctx* c) {
   (void)hipSetDevice(c->device);
   void* ptrs[] = {c->d_tips,  c->d_w,     c->d_prog,    c->d_gpos,    c->d_mat_branch, c->d_pmat,
                   c->d_eig,   c->d_inner, c->d_model,   c->d_blens,   c->d_out,        c->d_site,
-                  c->d_scratch, c->d_dstk, c->d_gslot,  c->d_sslot, c->d_grows, c->d_in, c->d_qprog, c->d_qscr};
+                  c->d_scratch, c->d_dstk, c->d_gslot,  c->d_sslot, c->d_grows, c->d_in, c->d_qprog, c->d_qscr,
+                  c->d_qfpart, c->d_qfcnt};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   if (c->h_in) (void)hipHostFree(c->h_in);
@@ -2663,6 +2909,18 @@ int launch_quad(phy_ctx* ctx, int n, const double* d_blens, const double* d_mode
     }
     ++ctx->plan_gen;
   }
+  // the split epilogue (qfin_kernel): items of bper branches x C categories per workgroup
+  const int bper = std::max(1, std::min((B + 15) / 16, QFIN_ITEMS / C));
+  const int nspl = (B + bper - 1) / bper;
+  if (!ctx->d_qfcnt) {  // once per context: hand-offs and zeroed tickets for QUAD_MAX_DRAWS draws
+    HIP_TRY(hipDeviceSynchronize());
+    int rc = dalloc(&ctx->d_qfpart, (size_t)QUAD_MAX_DRAWS * nspl * (16 + C));
+    if (!rc) rc = dalloc(&ctx->d_qfcnt, (size_t)QUAD_MAX_DRAWS);
+    if (rc) return rc;
+    HIP_TRY(hipMemset(ctx->d_qfcnt, 0, (size_t)QUAD_MAX_DRAWS * sizeof(unsigned long long)));
+    HIP_TRY(hipDeviceSynchronize());
+    ++ctx->plan_gen;
+  }
   QuadArgs qa;
   qa.s = SweepArgs{ctx->d_tips,  ctx->d_w,     ctx->d_pmat,  d_model,      ctx->d_scratch, ctx->d_dstk,
                    ctx->d_gslot, ctx->d_sslot, d_site,       d_out,        ctx->d_mat_branch, ctx->eig_cur,
@@ -2687,6 +2945,13 @@ int launch_quad(phy_ctx* ctx, int n, const double* d_blens, const double* d_mode
   FinArgs fa{ctx->d_gslot, ctx->d_sslot, ctx->d_pmat, ctx->eig_cur, d_blens, d_model, ctx->d_gpos, ctx->d_inner, d_out,
              C,            B,            ctx->nmat,   gx,          phy_output_len(ctx), 0, ctx->R, grows, gstride,
              ctx->kind,    gsum_in,      ctx->qfuse_pref ? 1 : 0};
+  if (gx <= QFIN_SLOTS && C * bper <= QFIN_ITEMS && 8 * C <= 128 && ctx->qfuse_pref) {
+    hipLaunchKernelGGL(qfin_kernel, dim3(nspl, n), dim3(QFIN_THREADS), 0, st,
+                       QfinArgs{fa, ctx->d_qfpart, ctx->d_qfcnt, bper, nspl});
+    HIP_TRY(hipGetLastError());
+    *qdone = true;
+    return PHY_OK;
+  }
   if (!gsum_in) {
     hipLaunchKernelGGL(gsum_kernel, dim3((C * B * 16 + 63) / 64, n), dim3(256), 0, st, fa);
     HIP_TRY(hipGetLastError());
