@@ -2131,6 +2131,7 @@ struct phy_ctx {
   size_t quad_lds = 0;
   int* d_qprog = nullptr;      // unpacked program, nothing rebuilt (every moved partial stored)
   double* d_qscr = nullptr;    // [wg][nslots][C][64]
+  bool quad_build = false;     // this launch's quad sweep builds its matrix records (no pmat launch)
   double* d_qfpart = nullptr;  // qfin_kernel hand-offs [QUAD_MAX_DRAWS][nspl][16 + C]
   unsigned long long* d_qfcnt = nullptr;  // its tickets [QUAD_MAX_DRAWS]
   long qscr_wgs = 0;
@@ -2723,6 +2724,10 @@ int launch_class(phy_ctx* ctx, int n, const double* d_blens, const double* d_mod
 
 int launch_pattern(phy_ctx* ctx, int n, const double* d_blens, const double* d_model, double* d_out,
                    double* d_site, hipStream_t st, double* grows, long long gstride, bool* qdone = nullptr);
+// the pattern engine takes the quad sweep for this call (launch_pattern)
+bool quad_applies(const phy_ctx* ctx, int n) {
+  return ctx->quad_ok && ctx->quad_pref && ctx->cols_pref == 0 && n <= QUAD_MAX_DRAWS;
+}
 
 // Returns whether the finalize ran the Q-parameter chain rule too: when its
 // LDS ([C][B] inner products, Q, the reduction rows and the chain rule's
@@ -2771,7 +2776,9 @@ int launch(phy_ctx* ctx, int n, const double* d_blens, const double* d_model, do
            double* d_site, hipStream_t st, const double* d_eig_in = nullptr) {
   const int C = ctx->C, B = ctx->B;
   ctx->eig_cur = d_eig_in ? d_eig_in : ctx->d_eig;
-  {
+  // the quad sweep builds its own records when the eigensystems are given
+  ctx->quad_build = d_eig_in && ctx->engine == 0 && quad_applies(ctx, n);
+  if (!ctx->quad_build) {
     // eigensystems: given (host-formed, the small host-buffer path); small
     // device batches: each pmat wave forms its draw's (one launch less);
     // large ones: one thread per draw first
@@ -2929,6 +2936,8 @@ int launch_quad(phy_ctx* ctx, int n, const double* d_blens, const double* d_mode
                    B,            phy_output_len(ctx), 0, ctx->extra, 0, d_blens, grows, gstride, 0, ctx->kind};
   qa.qscr = ctx->d_qscr;
   qa.nblk = nb;
+  qa.pmat_out = ctx->d_pmat;
+  qa.build = ctx->quad_build ? 1 : 0;
   hipEvent_t e0 = nullptr, e1 = nullptr;
   if (ctx->timing) {
     int rc = timing_begin(ctx, st, &e0, &e1);
@@ -2966,7 +2975,7 @@ int launch_pattern(phy_ctx* ctx, int n, const double* d_blens, const double* d_m
                    double* d_site, hipStream_t st, double* grows, long long gstride, bool* qdone) {
   const int C = ctx->C, B = ctx->B;
   // (an explicit column plan, phy_set_tuning(cols > 0), keeps the one / two column sweeps)
-  if (ctx->quad_ok && ctx->quad_pref && ctx->cols_pref == 0 && n <= QUAD_MAX_DRAWS && qdone)
+  if (quad_applies(ctx, n) && qdone)
     return launch_quad(ctx, n, d_blens, d_model, d_out, d_site, st, grows, gstride, qdone);
   // persistent workgroups: the explicit budget, else exactly what is resident
   const int budget = ctx->wg_budget > 0 ? ctx->wg_budget : ctx->wg_resident;
@@ -3274,7 +3283,7 @@ int phy_create(int S, int P, int C, int rooted, int model, const uint8_t* tipcod
   TRY_C(plan_chunks(c));
   {  // the quad sweep's program: every moved partial stored (no rebuilt cherries)
     c->quad_lds = quad_lds_bytes(S, C, c->nmat, c->R, c->ndeep);
-    c->quad_ok = c->quad_lds <= LDS_CAP;
+    c->quad_ok = c->quad_lds + EIG_LEN * sizeof(double) <= LDS_CAP;  // + qsweep_kernel's static eigensystem copy
     if (c->quad_ok) {
       std::vector<int> qp = c->prog;
       for (int s = 0; s < c->nsteps; ++s) {

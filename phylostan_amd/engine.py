@@ -242,17 +242,46 @@ class TreeLikelihood:
             mode = {"auto": 0, "pattern": 1, "class": 2, "resident": 3}[mode]
         _lib.check(self.lib.phy_set_engine(self.ctx, int(mode)), "phy_set_engine")
 
-    def prefer_latency_engine(self):
+    def prefer_latency_engine(self, probe=True, calls=24):
         """For host-driven samplers (a few draws per call, one call per
-        leapfrog / ELBO round): the resident class sweep when the tree is
-        rooted and its class state fits in LDS -- lower latency per small
-        batch (round 3, one box: fluA 4 draws 135 us against 139-141 us per
-        call, HCV 97-103 against 132-135) -- else the automatic
-        engine.  Returns the name."""
+        leapfrog / ELBO round): the faster of the pattern sweep (the quad
+        sweep for <= 16 draws) and the resident class sweep (when the tree is
+        rooted and its class state fits in LDS), measured here: ``calls``
+        synchronous calls of ``max_draws`` synthetic draws (branch lengths
+        0.05, uniform frequencies, unit rates) on each, in two alternating
+        rounds, the lower median kept.  One box, 4 draws (r04g/h): fluA quad
+        112 against resident 137 us per call, HCV 106 against 97 -- neither
+        wins everywhere, so it is measured, not guessed.  The choice affects
+        speed only: both engines pass the same parity tests (results agree to
+        the parity tolerances, not bitwise).  probe=False: the resident sweep
+        when it applies (round 3's rule).  Without the resident sweep: the
+        automatic engine.  Returns the name; the timings (us per call) are in
+        ``self.latency_probe``."""
         try:
             self.set_engine("resident")
         except _lib.PhyloHipError:
             self.set_engine("auto")
+            return self.engine()
+        if not probe:
+            return self.engine()
+        import time
+        n = self.max_draws
+        bl = np.full((n, self.B), 0.05)
+        mv = np.repeat(self.model_vector([0.25] * 4, [1.0] * 6, [1.0] * self.C, [1.0 / self.C] * self.C)[None], n,
+                       axis=0)
+        times = {"pattern": [], "resident": []}
+        for rnd in range(2):
+            for name in ("pattern", "resident"):
+                self.set_engine(name)
+                for _ in range(3):
+                    self.evaluate_rows(bl, mv)
+                for _ in range(calls // 2):
+                    t0 = time.perf_counter()
+                    self.evaluate_rows(bl, mv)
+                    times[name].append(time.perf_counter() - t0)
+        med = {k: 1e6 * float(np.median(v)) for k, v in times.items()}
+        self.latency_probe = med
+        self.set_engine(min(med, key=med.get))
         return self.engine()
 
     def engine(self):

@@ -110,3 +110,22 @@ def test_quad_impossible_draw_is_minus_inf(monkeypatch):
     rows = eng.evaluate_rows(bl2, mv)
     assert rows[1, 0] == -np.inf
     assert np.array_equal(rows[0], good[0]) and np.array_equal(rows[2], good[2])
+
+
+def test_prefer_latency_engine_measures_and_keeps_the_faster(monkeypatch):
+    """prefer_latency_engine times the pattern (quad) and resident sweeps on
+    synthetic draws and keeps the faster; the kept engine's rows agree with
+    the column sweeps'."""
+    case = cases.fluA_case()
+    n = 4
+    bl, mv = _draws(case, n, 21)
+    eng = _engine(case, max_draws=n, monkeypatch=monkeypatch)
+    name = eng.prefer_latency_engine()
+    assert set(eng.latency_probe) == {"pattern", "resident"}
+    assert name == min(eng.latency_probe, key=eng.latency_probe.get)
+    assert all(0.0 < t < 1e5 for t in eng.latency_probe.values())
+    rows = eng.evaluate_rows(bl, mv)
+    ref = _engine(case, max_draws=n, quad=False, monkeypatch=monkeypatch).evaluate_rows(bl, mv)
+    for k in range(n):
+        assert abs(rows[k, 0] - ref[k, 0]) <= RTOL_LL * abs(ref[k, 0])
+        _close(rows[k, 1:], ref[k, 1:], RTOL_G, "row %d" % k)
