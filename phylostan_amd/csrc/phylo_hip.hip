@@ -3194,7 +3194,13 @@ int phy_create(int S, int P, int C, int rooted, int model, const uint8_t* tipcod
     (void)hipFuncSetAttribute((const void*)res_fwd_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)LDS_CAP);
     (void)hipFuncSetAttribute((const void*)res_rev_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)LDS_CAP);
     (void)hipFuncSetAttribute((const void*)finalize_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)LDS_CAP);
-    (void)hipFuncSetAttribute((const void*)qsweep_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)LDS_CAP);
+    {  // its static eigensystem copy counts against the cap too
+      hipFuncAttributes fa{};
+      const size_t stat = hipFuncGetAttributes(&fa, (const void*)qsweep_kernel) == hipSuccess ? fa.sharedSizeBytes
+                                                                                                : 1024;
+      (void)hipFuncSetAttribute((const void*)qsweep_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                (int)(LDS_CAP - stat));
+    }
   }
   if (((size_t)C * c->B + 16 + 1024) * sizeof(double) > LDS_CAP) {
     delete c;
