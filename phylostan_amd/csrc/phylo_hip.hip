@@ -2946,7 +2946,8 @@ int launch_quad(phy_ctx* ctx, int n, const double* d_blens, const double* d_mode
   {
     const int* prog = ctx->d_qprog;
     void* kargs[] = {(void*)&qa, (void*)&prog};
-    HIP_TRY(hipLaunchKernel((const void*)qsweep_kernel, dim3(gx, n), dim3(C * WAVE), kargs, ctx->quad_lds, st));
+    const void* kern = C <= 4 ? (const void*)qsweep_kernel<256> : (const void*)qsweep_kernel<1024>;
+    HIP_TRY(hipLaunchKernel(kern, dim3(gx, n), dim3(C * WAVE), kargs, ctx->quad_lds, st));
   }
   HIP_TRY(hipGetLastError());
   if (ctx->timing) HIP_TRY(hipEventRecord(e1, st));
@@ -3194,12 +3195,10 @@ int phy_create(int S, int P, int C, int rooted, int model, const uint8_t* tipcod
     (void)hipFuncSetAttribute((const void*)res_fwd_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)LDS_CAP);
     (void)hipFuncSetAttribute((const void*)res_rev_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)LDS_CAP);
     (void)hipFuncSetAttribute((const void*)finalize_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)LDS_CAP);
-    {  // its static eigensystem copy counts against the cap too
-      hipFuncAttributes fa{};
-      const size_t stat = hipFuncGetAttributes(&fa, (const void*)qsweep_kernel) == hipSuccess ? fa.sharedSizeBytes
-                                                                                                : 1024;
-      (void)hipFuncSetAttribute((const void*)qsweep_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                (int)(LDS_CAP - stat));
+    for (const void* kern : {(const void*)qsweep_kernel<256>, (const void*)qsweep_kernel<1024>}) {
+      hipFuncAttributes fa{};  // its static eigensystem copy counts against the cap too
+      const size_t stat = hipFuncGetAttributes(&fa, kern) == hipSuccess ? fa.sharedSizeBytes : 1024;
+      (void)hipFuncSetAttribute(kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)(LDS_CAP - stat));
     }
   }
   if (((size_t)C * c->B + 16 + 1024) * sizeof(double) > LDS_CAP) {
@@ -3291,11 +3290,7 @@ int phy_create(int S, int P, int C, int rooted, int model, const uint8_t* tipcod
     c->quad_lds = quad_lds_bytes(S, C, c->nmat, c->R, c->ndeep);
     c->quad_ok = c->quad_lds + EIG_LEN * sizeof(double) <= LDS_CAP;  // + qsweep_kernel's static eigensystem copy
     if (c->quad_ok) {
-      std::vector<int> qp = c->prog;
-      for (int s = 0; s < c->nsteps; ++s) {
-        qp[(size_t)s * STEP_INTS + ST_FLAGS] &= ~(F_NOSTORE | F_PREVREC);
-        qp[(size_t)s * STEP_INTS + ST_RD] = 0;
-      }
+      const std::vector<int> qp = quad_program(c->prog, c->nsteps, C, c->R);
       TRY_C(dalloc(&c->d_qprog, qp.size()));
       HIP_C(hipMemcpy(c->d_qprog, qp.data(), qp.size() * sizeof(int), hipMemcpyHostToDevice));
     }
