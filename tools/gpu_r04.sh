@@ -79,8 +79,8 @@ fi
 if want sq4; then  # SQ counters of the quad sweep on the 4-draw fluA call (separate --pmc passes)
   PMC_SCRIPT=tools/latency_probe.py PMC_KERNEL=qsweep timeout -k 10 600 python tools/pmc_sq.py \
     --workload fluA --draws 4 --engine pattern --calls 50 > $O/sq4_qsweep.json 2> $O/sq4_qsweep.err
-  PMC_SCRIPT=tools/latency_probe.py PMC_KERNEL=finalize timeout -k 10 600 python tools/pmc_sq.py \
-    --workload fluA --draws 4 --engine pattern --calls 50 > $O/sq4_finalize.json 2> $O/sq4_finalize.err
+  PMC_SCRIPT=tools/latency_probe.py PMC_KERNEL=qfin timeout -k 10 600 python tools/pmc_sq.py \
+    --workload fluA --draws 4 --engine pattern --calls 50 > $O/sq4_qfin.json 2> $O/sq4_qfin.err
   head -c 600 $O/sq4_qsweep.json
 fi
 echo done
