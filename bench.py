@@ -77,7 +77,7 @@ def parse():
 
 def kernel_source_hash():
     h = hashlib.sha1()
-    for name in ("phylo_hip.hip", "class_engine.inc", "resident_engine.inc"):
+    for name in ("phylo_hip.hip", "class_engine.inc", "resident_engine.inc", "quad_engine.inc", "multi_device.inc"):
         with open(os.path.join(ROOT, "phylostan_amd", "csrc", name), "rb") as fp:
             h.update(fp.read())
     return h.hexdigest()[:12]
@@ -543,7 +543,7 @@ def main():
 
     if info["engine"] == "class":
         alg = class_algorithmic_bytes(C, info["class_classes"], info["class_stage"], info["class_staged"], draws)
-        kernel_name = "class sweep: cls_fwd/cls_root/cls_red/cls_fix/cls_rev kernels, forward through reverse"
+        kernel_name = "class sweep: cls_clade_fwd/cls_fwd/cls_root/cls_red/cls_fix_list/cls_rev/cls_clade_rev kernels, forward through reverse"
     elif info["engine"] == "resident":
         alg = resident_algorithmic_bytes(C, B, info["resident_root_classes"], info["resident_record_vectors"],
                                          draws)

@@ -83,4 +83,14 @@ if want sq4; then  # SQ counters of the quad sweep on the 4-draw fluA call (sepa
     --workload fluA --draws 4 --engine pattern --calls 50 > $O/sq4_qfin.json 2> $O/sq4_qfin.err
   head -c 600 $O/sq4_qsweep.json
 fi
+if want pmc; then  # HBM traffic (FETCH / WRITE passes) and SQ counters of the timed kernels, fluA and synthetic
+  timeout -k 10 600 python tools/pmc_traffic.py --workload fluA > $O/pmc_traffic_fluA.log 2>&1 && tail -1 $O/pmc_traffic_fluA.log
+  timeout -k 10 600 python tools/pmc_sq.py --steps 3 --warmup 1 --no-cpu-baseline --no-sampler-latency \
+    > $O/sq_pattern_fluA.json 2> $O/sq_pattern_fluA.err && head -c 400 $O/sq_pattern_fluA.json
+  timeout -k 10 600 python tools/pmc_traffic.py --workload synthetic --engine class > $O/pmc_traffic_synth.log 2>&1 \
+    && tail -1 $O/pmc_traffic_synth.log
+  timeout -k 10 600 python tools/pmc_sq.py --workload synthetic --engine class --steps 3 --warmup 1 --no-cpu-baseline \
+    --no-sampler-latency > $O/sq_class_synthetic.json 2> $O/sq_class_synthetic.err && head -c 400 $O/sq_class_synthetic.json
+  cp profiles/pmc_traffic.json profiles/sq_counters.json $O/
+fi
 echo done

@@ -36,7 +36,7 @@ def main():
             continue
         # pattern sweep: average per sweep_kernel dispatch; class sweep: the
         # sum over one evaluation's cls_* dispatches (evaluations counted by
-        # cls_root_ll_kernel)
+        # cls_root_kernel)
         cls = "class" in bench_args
         only = os.environ.get("PMC_KERNEL")  # e.g. res_rev_kernel: that kernel's dispatches only
         acc, nev = {}, {}
@@ -47,13 +47,13 @@ def main():
                     if only not in name:
                         continue
                 elif cls:
-                    if "cls_" not in name or "gsum" in name or "site" in name:
+                    if "cls_" not in name or "epi" in name or "site" in name:
                         continue
                 elif "sweep_kernel" not in name:
                     continue
                 cn = row["Counter_Name"]
                 acc[cn] = acc.get(cn, 0.0) + float(row["Counter_Value"])
-                if only or not cls or "cls_root_ll_kernel" in name:
+                if only or not cls or "cls_root_kernel" in name:
                     nev[cn] = nev.get(cn, 0) + 1
         for cn, v in acc.items():
             out[cn] = v / max(nev.get(cn, 1), 1)

@@ -25,14 +25,15 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
 
-CLASS_KERNELS = ("cls_fwd_kernel", "cls_root_ll_kernel", "cls_root_rev_kernel", "cls_red_kernel",
-                 "cls_fix_kernel", "cls_rev_kernel")
+# the class sweep's timed region (phy_timing_*: forward through the last reverse level)
+CLASS_KERNELS = ("cls_clade_fwd_kernel", "cls_fwd_kernel", "cls_root_kernel", "cls_red_kernel", "cls_red_list_kernel",
+                 "cls_fix_list_kernel", "cls_rev_kernel", "cls_clade_rev_kernel")
 
 
 def run_pass(counter, out_dir, bench_args, engine):
     """Average per launch of the timed region: the sweep_kernel dispatch
     (pattern sweep) or the sum of one evaluation's class-sweep dispatches
-    (class sweep; evaluations counted by cls_root_ll_kernel dispatches)."""
+    (class sweep; evaluations counted by cls_root_kernel dispatches)."""
     cmd = ["rocprofv3", "--pmc", counter, "--kernel-trace", "-d", out_dir, "-o", "run",
            "--output-format", "csv", "--", sys.executable, os.path.join(ROOT, "bench.py")] + bench_args
     subprocess.run(cmd, check=True, stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL,
@@ -46,7 +47,7 @@ def run_pass(counter, out_dir, bench_args, engine):
             if engine == "class":
                 if any(k in name for k in CLASS_KERNELS):
                     total += float(r["Counter_Value"])
-                    n += "cls_root_ll_kernel" in name
+                    n += "cls_root_kernel" in name
             elif "sweep_kernel" in name:
                 total += float(r["Counter_Value"])
                 n += 1
