@@ -83,6 +83,16 @@ if want sq4; then  # SQ counters of the quad sweep on the 4-draw fluA call (sepa
     --workload fluA --draws 4 --engine pattern --calls 50 > $O/sq4_qfin.json 2> $O/sq4_qfin.err
   head -c 600 $O/sq4_qsweep.json
 fi
+if want shardn; then  # the shard-of-8 evaluation with batched draws (4 NUTS chains / 8 / 16 per call)
+  for d in 4 8 16; do
+    timeout -k 10 300 python bench.py --workload synthetic --shard-of 8 --draws $d --steps 50 --warmup 5 \
+      --no-cpu-baseline --json-out $O/bench_shard8_d$d.json > $O/bench_shard8_d$d.log 2>&1
+    python -c "import json;d=json.load(open('$O/bench_shard8_d$d.json'));print('shard8 draws=$d', d['value'], d['ms_per_step'])"
+  done
+  timeout -k 10 300 python bench.py --workload synthetic --draws 4 --steps 20 --warmup 3 --no-cpu-baseline \
+    --json-out $O/bench_synth_d4.json > $O/bench_synth_d4.log 2>&1
+  python -c "import json;d=json.load(open('$O/bench_synth_d4.json'));print('synth draws=4', d['value'], d['ms_per_step'])"
+fi
 if want pmc; then  # HBM traffic (FETCH / WRITE passes) and SQ counters of the timed kernels, fluA and synthetic
   timeout -k 10 600 python tools/pmc_traffic.py --workload fluA > $O/pmc_traffic_fluA.log 2>&1 && tail -1 $O/pmc_traffic_fluA.log
   timeout -k 10 600 python tools/pmc_sq.py --steps 3 --warmup 1 --no-cpu-baseline --no-sampler-latency \
