@@ -93,6 +93,12 @@ if want shardn; then  # the shard-of-8 evaluation with batched draws (4 NUTS cha
     --json-out $O/bench_synth_d4.json > $O/bench_synth_d4.log 2>&1
   python -c "import json;d=json.load(open('$O/bench_synth_d4.json'));print('synth draws=4', d['value'], d['ms_per_step'])"
 fi
+if want profn; then  # kernel traces of the batched-draw class sweep (4 draws per call)
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof_shard8_d4 -o run -- \
+    python bench.py --workload synthetic --shard-of 8 --draws 4 --steps 30 --warmup 5 --no-cpu-baseline \
+    > $O/prof_shard8_d4.log 2>&1
+  python tools/prof_stats.py $O/prof_shard8_d4/run_results.db | head -16
+fi
 if want pmc; then  # HBM traffic (FETCH / WRITE passes) and SQ counters of the timed kernels, fluA and synthetic
   timeout -k 10 600 python tools/pmc_traffic.py --workload fluA > $O/pmc_traffic_fluA.log 2>&1 && tail -1 $O/pmc_traffic_fluA.log
   timeout -k 10 600 python tools/pmc_sq.py --steps 3 --warmup 1 --no-cpu-baseline --no-sampler-latency \
