@@ -1,4 +1,4 @@
-"""The committed bench lines (profiles/r03_*_bench.json) keep bench.py's
+"""The committed bench lines (profiles/r0N_*_bench.json, the latest round's) keep bench.py's
 contract: the driver's keys, a roofline whose fraction is its own
 achieved / peak and whose achieved rate is the algorithmic bytes over the
 kernel's average launch, a cpu_baseline with the fields the task names, and
@@ -9,7 +9,15 @@ import os
 import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-LINES = ["r03_fluA_bench.json", "r03_HCV_bench.json", "r03_DS1_bench.json", "r03_synthetic_class_bench.json"]
+def latest(kind):
+    """The newest round's committed line of this kind (r04_..., else r03_...)."""
+    for r in ("r04", "r03"):
+        if os.path.exists(os.path.join(ROOT, "profiles", "%s_%s" % (r, kind))):
+            return "%s_%s" % (r, kind)
+    raise FileNotFoundError(kind)
+
+
+LINES = [latest(k) for k in ("fluA_bench.json", "HCV_bench.json", "DS1_bench.json", "synthetic_class_bench.json")]
 KEYS = ["metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
         "vs_baseline", "dtype", "data", "config", "roofline", "cpu_baseline"]
 
@@ -41,7 +49,7 @@ def test_committed_bench_line_keeps_the_contract(name):
 def test_headline_metric_is_baselines():
     with open(os.path.join(ROOT, "BASELINE.json")) as f:
         base = json.load(f)
-    d = last_line("r03_fluA_bench.json")
+    d = last_line(latest("fluA_bench.json"))
     assert d["metric"] == base["metric"]
     assert d["nominal_check"]["ok"] is True
     # value: draws per step over the step time
@@ -49,8 +57,13 @@ def test_headline_metric_is_baselines():
 
 
 def test_pmc_traffic_belongs_to_the_committed_lines():
+    """A line reports the PMC traffic of its own kernel source only: equal to
+    the committed record when the sources match, null otherwise (bench.py
+    never prices a launch with another build's counters)."""
     with open(os.path.join(ROOT, "profiles", "pmc_traffic.json")) as f:
         pmc = json.load(f)
-    d = last_line("r03_fluA_bench.json")
-    assert d["kernel_source"] == pmc["kernel_source"]
-    assert d["roofline"]["traffic"] == pytest.approx(pmc["per_launch_bytes"]["fluA:8192:pattern"], rel=1e-12)
+    d = last_line(latest("fluA_bench.json"))
+    if d["kernel_source"] == pmc["kernel_source"]:
+        assert d["roofline"]["traffic"] == pytest.approx(pmc["per_launch_bytes"]["fluA:8192:pattern"], rel=1e-12)
+    else:
+        assert d["roofline"]["traffic"] is None

@@ -93,6 +93,12 @@ if want shardn; then  # the shard-of-8 evaluation with batched draws (4 NUTS cha
     --json-out $O/bench_synth_d4.json > $O/bench_synth_d4.log 2>&1
   python -c "import json;d=json.load(open('$O/bench_synth_d4.json'));print('synth draws=4', d['value'], d['ms_per_step'])"
 fi
+if want lines; then  # the committed bench lines: every dataset with its CPU baseline
+  for w in HCV DS1 synthetic; do
+    timeout -k 10 500 python bench.py --workload $w --json-out $O/bench_$w.json > $O/bench_$w.log 2>&1
+    python -c "import json;d=json.load(open('$O/bench_$w.json'));print('$w', d['value'], d['ms_per_step'], d['cpu_baseline']['value'])"
+  done
+fi
 if want profn; then  # kernel traces of the batched-draw class sweep (4 draws per call)
   timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof_shard8_d4 -o run -- \
     python bench.py --workload synthetic --shard-of 8 --draws 4 --steps 30 --warmup 5 --no-cpu-baseline \
