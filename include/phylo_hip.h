@@ -221,7 +221,10 @@ int phy_recomputed_partials(const phy_ctx* ctx);
  * phy_output_len follows. */
 int phy_set_output(phy_ctx* ctx, int compact);
 
-/* Engine: 1 = pattern sweep (one lane per pattern column), 2 = class sweep
+/* Engine: 1 = pattern sweep (one lane per pattern column; a call of at most
+ * 16 draws takes its quad form -- a quad of lanes per column, matrix records
+ * built in the sweep when the eigensystems are host-formed, an epilogue split
+ * over workgroups; PHY_QUAD=0 at phy_create keeps the column sweep), 2 = class sweep
  * (site repeats: the forward pass once per distinct tip-state tuple of each
  * subtree, the reverse on upper partials aggregated per tuple -- the exact,
  * total form of the reference's column-reuse cache, pruner/tree.cpp:140-174),
