@@ -41,6 +41,8 @@ CASES = {
     "caterpillar": lambda: cases.random_case(305, S=60, P=150, C=4, model="HKY", caterpillar=True),
     "P1": lambda: cases.random_case(306, S=9, P=1, C=2, model="GTR"),
     "all_ambiguous": lambda: cases.random_case(307, S=10, P=90, C=2, model="GTR", ambiguous=1.0),
+    # 94 blocks of 16 columns: a draw over more than 16 workgroups (qfin_kernel's batched slot sums)
+    "many_blocks": lambda: cases.random_case(308, S=30, P=1500, C=4, model="GTR"),
 }
 
 
@@ -51,7 +53,7 @@ def test_quad_single_eval_vs_oracle(name, monkeypatch):
     check_case(case, eng)
 
 
-@pytest.mark.parametrize("name", ["fluA", "HCV", "DS1", "rand_C3_GTR", "unrooted_C5", "rand_C16_HKY"])
+@pytest.mark.parametrize("name", ["fluA", "HCV", "DS1", "rand_C3_GTR", "unrooted_C5", "rand_C16_HKY", "many_blocks"])
 @pytest.mark.parametrize("n", [4, 16])
 def test_quad_batch_rows_equal_column_sweeps(name, n, monkeypatch):
     """The sampler's shape (host buffers, n draws per call, full rows):
