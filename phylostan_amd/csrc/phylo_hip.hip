@@ -1897,7 +1897,6 @@ struct QfinArgs {
   double* part;              // [draw][nspl][16 + C] hand-offs: M partial, sum_b b <G, QP> per category
   unsigned long long* cnt;   // [draw] tickets (modulo nspl; zeroed at allocation)
   int bper, nspl;
-  int p_by_branch;           // the P records are in branch order (the quad sweep built them), else matrix order
 };
 __global__ void __launch_bounds__(QFIN_THREADS) qfin_kernel(QfinArgs qa) {
   const FinArgs& a = qa.f;
@@ -1920,16 +1919,13 @@ __global__ void __launch_bounds__(QFIN_THREADS) qfin_kernel(QfinArgs qa) {
   const int li = tid >> 2, k = tid & 3;
   const int c = li / bper, bl = li - c * bper;
   const bool live = c < C && bl < nb;  // quad-uniform
-  const int b = b0 + (live ? bl : 0), idx = c * B + b;
-  const int mm = qa.p_by_branch ? b : a.gpos[b];  // the P record (the slots are by branch: quad_program)
-  // every global load of the item first (slots -- the first 16 -- and the P
-  // record), then the eigensystem's staging barrier: one memory round trip,
-  // not three; a draw over more than 16 workgroups sums the rest in batches
-  // of 16 after it (slot order throughout)
+  const int b = b0 + (live ? bl : 0), idx = c * B + b, mm = a.gpos[b];
+  // every global load of the item first (slots, P record), then the
+  // eigensystem's staging barrier: one memory round trip, not three
   double2 lo[QFIN_SLOTS], hi[QFIN_SLOTS], p01[4], p23[4];
-  const size_t per_wg = (size_t)C * a.nmat * 16;
-  const double* src = a.gslot + (size_t)draw * gx * per_wg + ((size_t)c * a.nmat + b) * 16 + k * 4;
   if (live) {
+    const size_t per_wg = (size_t)C * a.nmat * 16;
+    const double* src = a.gslot + (size_t)draw * gx * per_wg + ((size_t)c * a.nmat + mm) * 16 + k * 4;
 #pragma unroll
     for (int w = 0; w < QFIN_SLOTS; ++w)
       if (w < gx) {
@@ -1964,22 +1960,6 @@ __global__ void __launch_bounds__(QFIN_THREADS) qfin_kernel(QfinArgs qa) {
         r[2] += hi[w].x;
         r[3] += hi[w].y;
       }
-    for (int w0 = QFIN_SLOTS; w0 < gx; w0 += QFIN_SLOTS) {  // more than 16 workgroups per draw
-#pragma unroll
-      for (int w = 0; w < QFIN_SLOTS; ++w)
-        if (w0 + w < gx) {
-          lo[w] = *reinterpret_cast<const double2*>(src + (size_t)(w0 + w) * per_wg);
-          hi[w] = *reinterpret_cast<const double2*>(src + (size_t)(w0 + w) * per_wg + 2);
-        }
-#pragma unroll
-      for (int w = 0; w < QFIN_SLOTS; ++w)
-        if (w0 + w < gx) {
-          r[0] += lo[w].x;
-          r[1] += lo[w].y;
-          r[2] += hi[w].x;
-          r[3] += hi[w].y;
-        }
-    }
     double* grow = a.grows + (size_t)draw * a.grows_stride + (size_t)idx * 16 + k * 4;
     *reinterpret_cast<double2*>(grow) = make_double2(r[0], r[1]);
     *reinterpret_cast<double2*>(grow + 2) = make_double2(r[2], r[3]);
@@ -2975,13 +2955,19 @@ int launch_quad(phy_ctx* ctx, int n, const double* d_blens, const double* d_mode
   FinArgs fa{ctx->d_gslot, ctx->d_sslot, ctx->d_pmat, ctx->eig_cur, d_blens, d_model, ctx->d_gpos, ctx->d_inner, d_out,
              C,            B,            ctx->nmat,   gx,          phy_output_len(ctx), 0, ctx->R, grows, gstride,
              ctx->kind,    gsum_in,      ctx->qfuse_pref ? 1 : 0};
-  // the quad sweep's slots are by branch (quad_program): its epilogue is
-  // always qfin_kernel (C * bper <= QFIN_ITEMS by construction, C <= 16)
-  (void)gsum_in;
-  hipLaunchKernelGGL(qfin_kernel, dim3(nspl, n), dim3(QFIN_THREADS), 0, st,
-                     QfinArgs{fa, ctx->d_qfpart, ctx->d_qfcnt, bper, nspl, ctx->quad_build ? 1 : 0});
+  if (gx <= QFIN_SLOTS && C * bper <= QFIN_ITEMS && 8 * C <= 128 && ctx->qfuse_pref) {
+    hipLaunchKernelGGL(qfin_kernel, dim3(nspl, n), dim3(QFIN_THREADS), 0, st,
+                       QfinArgs{fa, ctx->d_qfpart, ctx->d_qfcnt, bper, nspl});
+    HIP_TRY(hipGetLastError());
+    *qdone = true;
+    return PHY_OK;
+  }
+  if (!gsum_in) {
+    hipLaunchKernelGGL(gsum_kernel, dim3((C * B * 16 + 63) / 64, n), dim3(256), 0, st, fa);
+    HIP_TRY(hipGetLastError());
+  }
+  *qdone = launch_finalize(fa, n, st);
   HIP_TRY(hipGetLastError());
-  *qdone = true;
   return PHY_OK;
 }
 
@@ -3304,7 +3290,7 @@ int phy_create(int S, int P, int C, int rooted, int model, const uint8_t* tipcod
     c->quad_lds = quad_lds_bytes(S, C, c->nmat, c->R, c->ndeep);
     c->quad_ok = c->quad_lds + EIG_LEN * sizeof(double) <= LDS_CAP;  // + qsweep_kernel's static eigensystem copy
     if (c->quad_ok) {
-      const std::vector<int> qp = quad_program(c->prog, c->nsteps, C, c->R, mat_branch);
+      const std::vector<int> qp = quad_program(c->prog, c->nsteps, C, c->R);
       TRY_C(dalloc(&c->d_qprog, qp.size()));
       HIP_C(hipMemcpy(c->d_qprog, qp.data(), qp.size() * sizeof(int), hipMemcpyHostToDevice));
     }
