@@ -223,14 +223,27 @@ bool forward(const Strict& m, const double* u, Draw& d) {
   d.logj = 0.0;
   if (m.weibull) ok &= lower(u[m.o_w], 0.1, d.w, d.ew, d.logj);
   d.props.resize(m.np);
-  for (int k = 0; k < m.np; ++k) {
-    // x = inv_logit(u), log|J| = -(log1p_exp(u) + log1p_exp(-u)): one exp
-    const double uu = u[m.o_props + k];
-    const double e = std::exp(-std::fabs(uu));
-    const double x = (uu >= 0.0 ? 1.0 : e) / (1.0 + e);
-    d.props[k] = x;
-    d.logj -= std::fabs(uu) + 2.0 * std::log1p(e);
-    ok &= std::isfinite(x) && x > 0.0 && x < 1.0;
+  {
+    // x = inv_logit(u), log|J| = -(log1p_exp(u) + log1p_exp(-u)) = -(|u| + 2 log(1 + e)),
+    // e = exp(-|u|): one exp per proportion, and the logs summed as the log of
+    // a product (each factor in (1, 2], renormalised every 512 factors)
+    double su = 0.0, prod = 1.0;
+    int pexp = 0;
+    for (int k = 0; k < m.np; ++k) {
+      const double uu = u[m.o_props + k];
+      const double e = std::exp(-std::fabs(uu));
+      const double x = (uu >= 0.0 ? 1.0 : e) / (1.0 + e);
+      d.props[k] = x;
+      su += std::fabs(uu);
+      prod *= 1.0 + e;
+      if ((k & 511) == 511) {
+        int ex;
+        prod = std::frexp(prod, &ex);
+        pexp += ex;
+      }
+      ok &= std::isfinite(x) && x > 0.0 && x < 1.0;
+    }
+    d.logj -= su + 2.0 * (std::log(prod) + pexp * 0.69314718055994530942);
   }
   if (m.est_rate) ok &= lower(u[m.o_rate], 0.0, d.rate, d.erate, d.logj);
   ok &= lower(u[m.o_height], m.lower_root, d.height, d.eheight, d.logj);
@@ -418,14 +431,22 @@ void phh_strict_post(void* hnd, int n, const double* U, const double* rows, int 
       l -= 1000.0 * d.rate;
       grate -= 1000.0;
     }
-    {  // log-Jacobian of the height transform
-      double s = 0.0;
+    {  // log-Jacobian of the height transform: sum log(gap) as the log of a
+       // product, renormalised every 8 gaps (no under- or overflow for gaps in
+       // [1e-38, 1e38]); a gap <= 0 gives -inf / NaN as the sum of logs does
+      double prod = 1.0;
+      int pexp = 0;
       for (size_t i = 0; i < m.jpar.size(); ++i) {
         const double gap = d.h[m.jpar[i]] - m.jlow[i];
-        s += std::log(gap);
+        prod *= gap;
+        if ((i & 7) == 7) {
+          int ex;
+          prod = std::frexp(prod, &ex);
+          pexp += ex;
+        }
         gh[m.jpar[i]] += 1.0 / gap;
       }
-      l += s;
+      l += std::log(prod) + pexp * 0.69314718055994530942;
     }
     if (m.coal) {  // constant coalescent, theta ~ oneOnX
       for (int i = 0; i < S; ++i) times[i] = m.tip_times[i];

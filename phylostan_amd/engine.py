@@ -147,33 +147,61 @@ class TreeLikelihood:
     def evaluate_rows(self, blens, model_vecs):
         """n draws -> the raw output rows [n, outlen] (no per-draw objects:
         the sampler's path)."""
-        blens = np.ascontiguousarray(np.atleast_2d(blens), dtype=np.float64)
-        mv = np.ascontiguousarray(np.atleast_2d(model_vecs), dtype=np.float64)
+        blens, mv = np.asarray(blens, np.float64), np.asarray(model_vecs, np.float64)
+        if blens.ndim == 1:
+            blens, mv = blens[None], mv.reshape(1, -1)
         n = blens.shape[0]
         if blens.shape != (n, self.B) or mv.shape != (n, self.model_len):
             raise ValueError("bad shapes: blens %s model %s" % (blens.shape, mv.shape))
+        if n <= min(self.max_draws, self._STAGE_DRAWS):  # a sampler's call: the staging arrays
+            sbl, smv, sout, pbl, pmv, pout = self._stage()
+            sbl[:n] = blens
+            smv[:n] = mv
+            _lib.check(self.lib.phy_eval(self.ctx, n, pbl, pmv, pout, None), "phy_eval")
+            return sout[:n].copy()
+        blens, mv = np.ascontiguousarray(blens), np.ascontiguousarray(mv)
         out = np.empty((n, self.outlen))
         _lib.check(self.lib.phy_eval(self.ctx, n, blens.ctypes.data, mv.ctypes.data, out.ctypes.data, None),
                    "phy_eval")
         return out
 
+    _STAGE_DRAWS = 128  # phy_eval_submit's batch limit (PIN_DRAWS)
+
+    def _stage(self):
+        """Host staging arrays of the submit / wait pair with their addresses
+        resolved once: ``ndarray.ctypes`` costs ~2.5 us a call, a sizeable part
+        of a sampler round's host time."""
+        if getattr(self, "_st", None) is None:
+            k = min(self.max_draws, self._STAGE_DRAWS)
+            bl, mv, out = np.empty((k, self.B)), np.empty((k, self.model_len)), np.empty((k, self.outlen))
+            self._st = (bl, mv, out, bl.ctypes.data, mv.ctypes.data, out.ctypes.data)
+        return self._st
+
     def submit_rows(self, blens, model_vecs):
-        """Start an evaluation of n <= 64 draws (phy_eval_submit) and return
+        """Start an evaluation of n <= 128 draws (phy_eval_submit) and return
         at once; ``wait_rows`` collects its raw output rows."""
-        blens = np.ascontiguousarray(np.atleast_2d(blens), dtype=np.float64)
-        mv = np.ascontiguousarray(np.atleast_2d(model_vecs), dtype=np.float64)
+        blens, mv = np.asarray(blens, np.float64), np.asarray(model_vecs, np.float64)
+        if blens.ndim == 1:
+            blens, mv = blens[None], mv.reshape(1, -1)
         n = blens.shape[0]
         if blens.shape != (n, self.B) or mv.shape != (n, self.model_len):
             raise ValueError("bad shapes: blens %s model %s" % (blens.shape, mv.shape))
-        _lib.check(self.lib.phy_eval_submit(self.ctx, n, blens.ctypes.data, mv.ctypes.data), "phy_eval_submit")
+        sbl, smv, _, pbl, pmv, _ = self._stage()
+        if n <= sbl.shape[0]:
+            sbl[:n] = blens  # phy_eval_submit stages them into pinned memory before it returns
+            smv[:n] = mv
+        else:  # beyond the limit: phy_eval_submit reports it
+            blens, mv = np.ascontiguousarray(blens), np.ascontiguousarray(mv)
+            pbl, pmv = blens.ctypes.data, mv.ctypes.data
+        _lib.check(self.lib.phy_eval_submit(self.ctx, n, pbl, pmv), "phy_eval_submit")
         self._pending = n
 
     def wait_rows(self):
         """The rows [n, outlen] of the evaluation ``submit_rows`` started."""
-        out = np.empty((self._pending, self.outlen))
-        self._pending = 0
-        _lib.check(self.lib.phy_eval_wait(self.ctx, out.ctypes.data), "phy_eval_wait")
-        return out
+        n, self._pending = self._pending, 0
+        _, _, out, _, _, pout = self._stage()
+        _lib.check(self.lib.phy_eval_wait(self.ctx, pout), "phy_eval_wait")
+        return out[:n].copy()
 
     def evaluate(self, blens, model_vec, site_ll=False):
         return self.evaluate_batch(blens, model_vec, site_ll)[0]
@@ -234,6 +262,7 @@ class TreeLikelihood:
         dL/dP block: 1 + B + 2C + 14 doubles per draw, what a sampler needs)."""
         _lib.check(self.lib.phy_set_output(self.ctx, int(bool(compact))), "phy_set_output")
         self.outlen = self.lib.phy_output_len(self.ctx)
+        self._st = None  # the staging rows follow the row length
 
     def set_engine(self, mode=0):
         """0 automatic, 1 pattern sweep, 2 class sweep (site repeats), 3 resident

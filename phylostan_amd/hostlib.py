@@ -46,6 +46,21 @@ def load():
             lib.phh_strict_pre.restype = ctypes.c_int
             lib.phh_strict_post.argtypes = [ctypes.c_void_p, _i, _D, _D, _i, _I, _i, _D, _D]
             lib.phh_strict_post.restype = None
+        if hasattr(lib, "phn_create"):
+            _f = ctypes.c_double
+            lib.phn_create.argtypes = [_i, _i, _D, _D, _i, _i, _i, _i, _f, _f, _f, _f, _f, _i, _i, _i, _f]
+            lib.phn_create.restype = ctypes.c_void_p
+            lib.phn_free.argtypes = [ctypes.c_void_p]
+            lib.phn_free.restype = None
+            lib.phn_step.argtypes = [ctypes.c_void_p, _i, _I, _D, _D, _D, _I]
+            lib.phn_step.restype = ctypes.c_int
+            lib.phn_error.argtypes = [ctypes.c_void_p, _i]
+            lib.phn_error.restype = ctypes.c_int
+            lib.phn_info.argtypes = [ctypes.c_void_p, _i, ctypes.POINTER(ctypes.c_long),
+                                     ctypes.POINTER(ctypes.c_double), _D]
+            lib.phn_info.restype = ctypes.c_int
+            lib.phn_draws.argtypes = [ctypes.c_void_p, _i, _D, _D]
+            lib.phn_draws.restype = None
         _lib = lib
     return _lib
 
@@ -137,30 +152,52 @@ class StrictPosterior:
             float(lower_root), dim, offs.ctypes.data, nat.m, nat.p_node, nat.p_par, nat.p_prop, nat.p_low, nat.root,
             nat.p_bpar, nat.p_bh, nat.p_blow, len(nat.jpar), nat.p_jpar, nat.p_jlow, self.lowers.ctypes.data)
         self._n = 0
+        self._rowlen = 0
+        self._last_u = None
 
+    # Work arrays with their addresses resolved once (``ndarray.ctypes`` costs
+    # ~2.5 us a call: nine of them were a fifth of a NUTS round's host time).
+    # pre / post copy their operands in and their results out.
     def _buffers(self, n):
         if n > self._n:
             self._n = n
+            self.U = np.empty((n, self.dim))
             self.blens = np.empty((n, self.B))
             self.mv = np.empty((n, self.ml))
             self.sel = np.empty(n, np.int32)
-        return self.blens, self.mv, self.sel
+            self.psel = np.empty(n, np.int32)
+            self.lp = np.empty(n)
+            self.G = np.empty((n, self.dim))
+            self.rows = np.empty((n, max(self._rowlen, 1)))
+            self._p = {k: getattr(self, k).ctypes.data for k in ("U", "blens", "mv", "sel", "psel", "lp", "G", "rows")}
+        return self._p
 
     def pre(self, U):
         """U [n, dim] -> (count, blens [count, B], model vectors [count, ml], sel [n])."""
         n = U.shape[0]
-        bl, mv, sel = self._buffers(n)
-        cnt = self.lib.phh_strict_pre(self.h, n, U.ctypes.data, bl.ctypes.data, mv.ctypes.data, sel.ctypes.data)
-        return cnt, bl[:cnt], mv[:cnt], sel[:n].copy()
+        p = self._buffers(n)
+        self.U[:n] = U
+        self._last_u = U
+        cnt = self.lib.phh_strict_pre(self.h, n, p["U"], p["blens"], p["mv"], p["sel"])
+        return cnt, self.blens[:cnt], self.mv[:cnt], self.sel[:n].copy()
 
     def post(self, U, rows, sel, need_grad=True):
         n = U.shape[0]
-        lp = np.empty(n)
-        G = np.empty((n, self.dim)) if need_grad else None
-        rows = _c(rows) if rows is not None and len(rows) else np.zeros((1, 1))
-        self.lib.phh_strict_post(self.h, n, U.ctypes.data, rows.ctypes.data, rows.shape[1], _c(sel, np.int32).ctypes.data,
-                                 int(need_grad), lp.ctypes.data, G.ctypes.data if need_grad else None)
-        return lp, G
+        p = self._buffers(n)
+        if U is not self._last_u:  # pre's draws are in self.U already (the begin / end pair)
+            self.U[:n] = U
+            self._last_u = None
+        rowlen = rows.shape[1] if rows is not None and len(rows) else 1
+        if rowlen != self.rows.shape[1]:  # the row length is the stride phh_strict_post reads with
+            self._rowlen = rowlen
+            self.rows = np.empty((self._n, rowlen))
+            p["rows"] = self.rows.ctypes.data
+        if rows is not None and len(rows):
+            self.rows[:len(rows)] = rows
+        self.psel[:n] = sel
+        self.lib.phh_strict_post(self.h, n, p["U"], p["rows"], rowlen, p["psel"], int(need_grad), p["lp"],
+                                 p["G"] if need_grad else None)
+        return self.lp[:n].copy(), (self.G[:n].copy() if need_grad else None)
 
     def __del__(self):
         if getattr(self, "h", None) and self.lib is not None:

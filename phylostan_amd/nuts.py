@@ -17,7 +17,9 @@ lockstep and evaluates the pending positions of all of them in ONE batched
 call (one GPU launch of ``n_chains`` draws), so 8 chains cost about as much
 wall time per leapfrog step as one.
 """
+import ctypes
 import math
+import os
 import time
 
 import numpy as np
@@ -369,15 +371,99 @@ class StaticHMCChain(Chain):
         return self
 
 
+_CHAIN_OPTIONS = dict(delta=0.8, gamma=0.05, kappa=0.75, t0=10.0, stepsize=1.0, init_buffer=75, term_buffer=50,
+                      base_window=25, max_delta_h=1000.0)  # Chain.__init__'s defaults
+
+
+class NativeChain:
+    """A finished chain of the native sampler, with ``Chain``'s result
+    attributes (draws, n_grad, eps, inv_metric)."""
+
+    def __init__(self, dim, draws, n_grad, eps, inv_metric):
+        self.dim, self.draws, self.n_grad, self.eps, self.inv_metric = dim, draws, n_grad, eps, inv_metric
+
+
+def native_available():
+    from . import hostlib
+    lib = hostlib.load()
+    return lib if lib is not None and hasattr(lib, "phn_create") else None
+
+
+def _run_native(lib, posterior, q0s, seeds, num_warmup, num_samples, thin, progress, max_depth, **kw):
+    """``Chain`` programs run by csrc/nuts_host.cpp (the same algorithm and
+    random streams; tests/test_nuts_native.py): one C call per gradient
+    round advances every chain and returns the positions of the next
+    batched ``posterior.log_prob_grad`` call."""
+    bad = set(kw) - set(_CHAIN_OPTIONS)
+    if bad:
+        raise TypeError("unexpected NUTS option(s) %s" % sorted(bad))
+    o = dict(_CHAIN_OPTIONS, **kw)
+    dim, n = posterior.dim, len(q0s)
+    rngs = [np.random.default_rng(sd) for sd in seeds]  # alive while the chains draw from them
+    bitgens = np.array([r.bit_generator.ctypes.bit_generator.value for r in rngs], np.uintp)
+    q0 = np.ascontiguousarray(np.stack([np.asarray(q, np.float64).reshape(dim) for q in q0s]))
+    h = lib.phn_create(n, dim, q0.ctypes.data, bitgens.ctypes.data, int(num_warmup), int(num_samples), int(thin),
+                       int(max_depth), float(o["delta"]), float(o["gamma"]), float(o["kappa"]), float(o["t0"]),
+                       float(o["stepsize"]), int(o["init_buffer"]), int(o["term_buffer"]), int(o["base_window"]),
+                       float(o["max_delta_h"]))
+    try:
+        # the round's arrays, addresses resolved once (ndarray.ctypes ~2.5 us)
+        Q, LP, GR = np.empty((n, dim)), np.empty(n), np.empty((n, dim))
+        idx_a, idx_b = np.empty(n, np.int32), np.empty(n, np.int32)
+        pQ, pLP, pGR = Q.ctypes.data, LP.ctypes.data, GR.ctypes.data
+        pa, pb = idx_a.ctypes.data, idx_b.ctypes.data
+        m = lib.phn_step(h, 0, None, None, None, pQ, pa)
+        rounds, t0 = 0, time.time()
+        while m > 0:
+            lp, G = posterior.log_prob_grad(Q[:m])
+            LP[:m] = lp
+            GR[:m] = G
+            pa, pb = pb, pa
+            m = lib.phn_step(h, m, pb, pLP, pGR, pQ, pa)
+            rounds += 1
+            if progress and rounds % 2000 == 0:
+                nd = lib.phn_info(h, 0, None, None, None)
+                progress("NUTS: %d gradient rounds, %d draws (chain 0), %.1f s" % (rounds, nd, time.time() - t0))
+        if m < 0:
+            code = lib.phn_error(h, -m - 1)
+            raise RuntimeError({1: "NUTS: initial point has non-finite log density",
+                                2: "NUTS: posterior is improper (step size > 1e7)",
+                                3: "NUTS: no acceptable small step size"}.get(code, "NUTS: chain failed (%d)" % code))
+        out = []
+        for c in range(n):
+            ng, eps = ctypes.c_long(), ctypes.c_double()
+            im = np.empty(dim)
+            nd = lib.phn_info(h, c, ctypes.byref(ng), ctypes.byref(eps), im.ctypes.data)
+            q, st = np.empty((nd, dim)), np.empty((nd, 8))
+            lib.phn_draws(h, c, q.ctypes.data, st.ctypes.data)
+            draws = [(q[k], float(s[0]), float(s[1]), float(s[2]), int(s[3]), int(s[4]), int(s[5]), float(s[6]),
+                      bool(s[7])) for k, s in enumerate(st)]
+            out.append(NativeChain(dim, draws, int(ng.value), float(eps.value), im))
+        return out
+    finally:
+        lib.phn_free(h)
+
+
 def run_chains(posterior, q0s, seeds, num_warmup=1000, num_samples=1000, thin=1, progress=None,
-               max_depth=10, algorithm="nuts", **kw):
+               max_depth=10, algorithm="nuts", native=None, **kw):
     """Run ``len(q0s)`` NUTS (or static HMC) chains in lockstep, batching
     every round of gradient requests into one ``posterior.log_prob_grad``
     call (one small-batch likelihood launch for all chains).  Every chain
     sees exactly the values it would see alone: evaluations are per draw,
     independent of the batch.  (Pipelining chain groups over two contexts
-    was measured slower -- the host's cost is per call -- and retired.)"""
+    was measured slower -- the host's cost is per call -- and retired.)
+
+    NUTS runs on the native chains (csrc/nuts_host.cpp) when libphylo_host.so
+    has them, unless ``native=False`` or ``PHYLO_NUTS=python``; the
+    generators below are their specification."""
     dim = posterior.dim
+    if native is None:
+        native = os.environ.get("PHYLO_NUTS", "native") != "python"
+    lib = native_available() if native and algorithm != "hmc" else None
+    if native and algorithm != "hmc" and lib is None and os.environ.get("PHYLO_NUTS") == "native":
+        raise RuntimeError("PHYLO_NUTS=native but libphylo_host.so has no NUTS chains (run build())")
+    if lib is not None:
+        return _run_native(lib, posterior, q0s, seeds, num_warmup, num_samples, thin, progress, max_depth, **kw)
     if algorithm == "hmc":
         chains = [StaticHMCChain(dim, q0, np.random.default_rng(sd), num_warmup, num_samples, thin, **kw)
                   for q0, sd in zip(q0s, seeds)]

@@ -1,0 +1,122 @@
+"""CPU: the native NUTS chains (csrc/nuts_host.cpp) against nuts.py's
+generator chains, their specification: the same seeds give bitwise the same
+draws, statistics, gradient counts, step sizes and metrics (dimensions below
+16, where numpy's dot is one fused multiply-add chain and the native dot
+follows it), through warmup windows, divergences, out-of-support positions,
+thinning and short warmups; longer vectors agree to rounding."""
+import numpy as np
+import pytest
+
+from phylostan_amd import nuts
+
+pytestmark = pytest.mark.skipif(nuts.native_available() is None, reason="libphylo_host.so without NUTS chains")
+
+
+class Gauss:
+    """Independent normals (lp, grad); ``trunc``: lp = -inf below it in x0."""
+
+    def __init__(self, sd, trunc=None, nan_grad_below=None):
+        self.sd = np.asarray(sd, np.float64)
+        self.dim = self.sd.size
+        self.trunc, self.nan_below = trunc, nan_grad_below
+
+    def log_prob_grad(self, U):
+        U = np.atleast_2d(U)
+        lp = -0.5 * ((U / self.sd) ** 2).sum(1)
+        G = -U / self.sd ** 2
+        if self.trunc is not None:
+            lp = np.where(U[:, 0] < self.trunc, -np.inf, lp)
+        if self.nan_below is not None:
+            G = np.where((U[:, :1] < self.nan_below), np.nan, G)
+        return lp, G
+
+
+def _pair(tgt, n_chains=3, **kw):
+    q0s = [np.full(tgt.dim, 0.3 * k) for k in range(n_chains)]
+    seeds = [(5, k) for k in range(n_chains)]
+    return (nuts.run_chains(tgt, q0s, seeds, native=False, **kw),
+            nuts.run_chains(tgt, q0s, seeds, native=True, **kw))
+
+
+def _assert_same(a, b):
+    assert len(a) == len(b)
+    for ca, cb in zip(a, b):
+        assert isinstance(cb, nuts.NativeChain)
+        assert len(ca.draws) == len(cb.draws)
+        assert ca.n_grad == cb.n_grad and ca.eps == cb.eps
+        np.testing.assert_array_equal(ca.inv_metric, cb.inv_metric)
+        for da, db in zip(ca.draws, cb.draws):
+            np.testing.assert_array_equal(da[0], db[0])
+            assert da[1:] == db[1:]
+            assert [type(x) for x in da[1:]] == [type(x) for x in db[1:]]
+
+
+@pytest.mark.parametrize("name,sd,kw", [
+    ("1d", [2.0], dict(num_warmup=300, num_samples=300)),
+    ("2d-aniso", [1.0, 30.0], dict(num_warmup=300, num_samples=200)),
+    ("5d", [1, 3, 0.1, 10, 0.5], dict(num_warmup=250, num_samples=100)),
+    ("12d", list(np.linspace(0.2, 5, 12)), dict(num_warmup=200, num_samples=100)),
+    ("stiff-divergent", [1e-3, 1e3], dict(num_warmup=150, num_samples=50, max_depth=6)),
+    ("short-warmup-thin", [1.0, 2.0], dict(num_warmup=15, num_samples=20, thin=3)),
+    ("no-warmup", [1.0, 2.0, 3.0], dict(num_warmup=0, num_samples=40)),
+    ("options", [1.0, 2.0], dict(num_warmup=120, num_samples=30, delta=0.95, stepsize=0.1, max_delta_h=5.0,
+                                  init_buffer=10, term_buffer=10, base_window=5)),
+])
+def test_native_chains_bitwise_equal_to_generators(name, sd, kw):
+    a, b = _pair(Gauss(sd), **kw)
+    _assert_same(a, b)
+
+
+def test_native_chains_out_of_support_and_nan_gradients():
+    """lp = -inf regions (divergent leaves, rejected steps) and non-finite
+    gradients (zeroed) take the same branches."""
+    a, b = _pair(Gauss([1.0, 0.5], trunc=-0.4), num_warmup=150, num_samples=150)
+    _assert_same(a, b)
+    assert sum(d[6] for c in a for d in c.draws) > 0
+    a, b = _pair(Gauss([1.0, 0.5], nan_grad_below=-1.5), num_warmup=100, num_samples=100)
+    _assert_same(a, b)
+
+
+def test_native_chains_long_vectors_agree_to_rounding():
+    """40 dimensions: numpy's dot vectorises, the draws agree to rounding
+    while the trajectories stay short-lived (first draws)."""
+    a, b = _pair(Gauss(np.linspace(0.5, 2.0, 40)), n_chains=2, num_warmup=0, num_samples=3)
+    for ca, cb in zip(a, b):
+        assert [d[4:7] for d in ca.draws] == [d[4:7] for d in cb.draws]
+        for da, db in zip(ca.draws, cb.draws):
+            np.testing.assert_allclose(db[0], da[0], rtol=1e-10, atol=1e-12)
+
+
+def test_native_chains_sample_the_target():
+    """Moments of a 3-d Gaussian from the native sampler alone."""
+    sd = np.array([0.5, 2.0, 4.0])
+    ch = nuts.run_chains(Gauss(sd), [np.zeros(3), np.ones(3)], [4, 5], num_warmup=500, num_samples=2000,
+                         native=True)
+    X = np.concatenate([np.stack([d[0] for d in c.draws if not d[8]]) for c in ch])
+    np.testing.assert_allclose(X.std(0), sd, rtol=0.1)
+    np.testing.assert_allclose(X.mean(0), 0.0, atol=0.15 * sd.max())
+
+
+def test_native_chains_errors_match():
+    tgt = Gauss([1.0, 1.0], trunc=0.5)
+    for native in (False, True):
+        with pytest.raises(RuntimeError, match="initial point has non-finite log density"):
+            nuts.run_chains(tgt, [np.zeros(2)], [1], num_warmup=10, num_samples=10, native=native)
+    with pytest.raises(TypeError):
+        nuts.run_chains(Gauss([1.0]), [np.zeros(1)], [1], num_warmup=10, num_samples=10, native=True, bogus=1)
+
+
+class Flat:
+    """A flat density: init_stepsize keeps doubling until the step size
+    passes 1e7 ("posterior is improper")."""
+    dim = 2
+
+    def log_prob_grad(self, U):
+        U = np.atleast_2d(U)
+        return np.zeros(U.shape[0]), np.zeros_like(U)
+
+
+def test_native_chains_improper_posterior():
+    for native in (False, True):
+        with pytest.raises(RuntimeError, match="improper"):
+            nuts.run_chains(Flat(), [np.zeros(2)], [1], num_warmup=10, num_samples=10, native=native)
