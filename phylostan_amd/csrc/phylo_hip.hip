@@ -2178,6 +2178,11 @@ struct phy_ctx {
   // eigensystems of up to 32 draws are formed on the host (stage_small) and ride along
   double* h_in = nullptr;   // pinned [PIN_DRAWS][B + model_len + EIG_LEN]
   double* h_out = nullptr;  // pinned [PIN_DRAWS][full output row]
+  // the small path's kernel-side views of h_in / h_out when the kernels read
+  // their operands from / write their rows to pinned host memory directly
+  // (PHY_DIRECT_IN / PHY_DIRECT_OUT), else nullptr: blits through d_in / d_out
+  const double* h_in_dev = nullptr;
+  double* h_out_dev = nullptr;
   double* d_in = nullptr;   // device [PIN_DRAWS][B + model_len + EIG_LEN]
   int pending = 0;          // draws of a phy_eval_submit not yet collected by phy_eval_wait
   double2* d_scratch = nullptr;
@@ -2423,6 +2428,16 @@ constexpr size_t LDS_CAP = 160 * 1024;
 #include "resident_engine.inc"
 constexpr int PIN_DRAWS = 128;  // phy_eval batches up to this size go through pinned staging
                                 // (ADVI's elbo_samples = 100 fits: phylostan.py:47)
+#ifndef PHY_DIRECT_OUT_DEFAULT
+#define PHY_DIRECT_OUT_DEFAULT 0
+#endif
+#ifndef PHY_DIRECT_IN_DEFAULT
+#define PHY_DIRECT_IN_DEFAULT 0
+#endif
+bool env_flag(const char* name, int dflt) {
+  const char* v = getenv(name);
+  return v ? atoi(v) != 0 : dflt != 0;
+}
 constexpr int MIN_CAP = 24;  // an occupancy level is taken only if chunks stay this large
 
 int nblk_for(int P, int K) { return (P + WAVE * K - 1) / (WAVE * K); }
@@ -2676,10 +2691,11 @@ int launch_class(phy_ctx* ctx, int n, const double* d_blens, const double* d_mod
     a.count = L.nchunk;
     hipLaunchKernelGGL(cls_fwd_kernel, dim3((L.nchunk + 3) / 4, dcn), dim3(256), 0, st, a);
   }
-  if (C <= 4)
-    hipLaunchKernelGGL(cls_root_kernel<256>, dim3(e->nrootch, n), dim3(C * WAVE), 0, st, a);
-  else
-    hipLaunchKernelGGL(cls_root_kernel<1024>, dim3(e->nrootch, n), dim3(C * WAVE), 0, st, a);
+  {
+    auto rk = C <= 4 ? (e->root_tips ? cls_root_kernel<256, true> : cls_root_kernel<256, false>)
+                     : (e->root_tips ? cls_root_kernel<1024, true> : cls_root_kernel<1024, false>);
+    hipLaunchKernelGGL(rk, dim3(e->nrootch, n), dim3(C * WAVE), 0, st, a);
+  }
   for (int l = e->levels - 1; l > e->Lc; --l) {
     const ClassLevel& L = e->lv[l];
     if (L.ntile) {
@@ -3248,6 +3264,16 @@ int phy_create(int S, int P, int C, int rooted, int model, const uint8_t* tipcod
     TRY_C(dalloc(&c->d_in, pin * (c->B + 10 + 2 * C + EIG_LEN)));
     HIP_C(hipHostMalloc((void**)&c->h_in, sizeof(double) * pin * (c->B + 10 + 2 * C + EIG_LEN), hipHostMallocDefault));
     HIP_C(hipHostMalloc((void**)&c->h_out, sizeof(double) * pin * outlen_full, hipHostMallocDefault));
+    if (env_flag("PHY_DIRECT_OUT", PHY_DIRECT_OUT_DEFAULT)) {
+      void* dp = nullptr;
+      HIP_C(hipHostGetDevicePointer(&dp, c->h_out, 0));
+      c->h_out_dev = static_cast<double*>(dp);
+    }
+    if (env_flag("PHY_DIRECT_IN", PHY_DIRECT_IN_DEFAULT)) {
+      void* dp = nullptr;
+      HIP_C(hipHostGetDevicePointer(&dp, c->h_in, 0));
+      c->h_in_dev = static_cast<const double*>(dp);
+    }
   }
   {
     // tip nibbles: record vector of the pattern's mask (R <= 16); padding =
@@ -3442,6 +3468,24 @@ int phy_eval_device(phy_ctx* ctx, int n_draws, const double* d_blens, const doub
                         [&]() -> int { return launch(ctx, n_draws, d_blens, d_model, d_out, d_site_ll, st); });
 }
 
+// The small-batch path's launches: inputs staged in h_in (stage_small),
+// rows to h_out.  With PHY_DIRECT_IN / PHY_DIRECT_OUT the kernels read the
+// staged inputs from / write the rows to pinned host memory themselves
+// instead of a blit each way.
+int launch_small(phy_ctx* ctx, int n_draws, size_t nin, size_t nb, size_t nm, size_t no, bool heig, double* dsite,
+                 hipStream_t st) {
+  const double* in = ctx->h_in_dev;
+  if (!in) {
+    HIP_TRY(hipMemcpyAsync(ctx->d_in, ctx->h_in, sizeof(double) * nin, hipMemcpyHostToDevice, st));
+    in = ctx->d_in;
+  }
+  double* out = ctx->h_out_dev ? ctx->h_out_dev : ctx->d_out;
+  int r = launch(ctx, n_draws, in, in + nb, out, dsite, st, heig ? in + nb + nm : nullptr);
+  if (r) return r;
+  if (!ctx->h_out_dev) HIP_TRY(hipMemcpyAsync(ctx->h_out, ctx->d_out, sizeof(double) * no, hipMemcpyDeviceToHost, st));
+  return PHY_OK;
+}
+
 // phy_eval_submit / phy_eval_wait: the small-batch path split at the stream
 // synchronisation, so a host can overlap its own work (or another context's
 // GPU work) with this evaluation.
@@ -3469,12 +3513,7 @@ int phy_eval_submit(phy_ctx* ctx, int n_draws, const double* blens, const double
   bool heig = false;
   const size_t nin = stage_small(ctx, n_draws, blens, model, &heig);
   int rc = launch_graphed(ctx, n_draws, ctx->h_in, ctx->d_in, ctx->h_out, nullptr, st, [&]() -> int {
-    HIP_TRY(hipMemcpyAsync(ctx->d_in, ctx->h_in, sizeof(double) * nin, hipMemcpyHostToDevice, st));
-    int r = launch(ctx, n_draws, ctx->d_in, ctx->d_in + nb, ctx->d_out, nullptr, st,
-                   heig ? ctx->d_in + nb + nm : nullptr);
-    if (r) return r;
-    HIP_TRY(hipMemcpyAsync(ctx->h_out, ctx->d_out, sizeof(double) * no, hipMemcpyDeviceToHost, st));
-    return PHY_OK;
+    return launch_small(ctx, n_draws, nin, nb, nm, no, heig, nullptr, st);
   });
   if (rc) return rc;
   ctx->pending = n_draws;
@@ -3517,12 +3556,7 @@ int phy_eval(phy_ctx* ctx, int n_draws, const double* blens, const double* model
     const size_t nin = stage_small(ctx, n_draws, blens, model, &heig);
     double* dsite = site_ll ? ctx->d_site : nullptr;
     int rc = launch_graphed(ctx, n_draws, ctx->h_in, ctx->d_in, ctx->h_out, dsite, st, [&]() -> int {
-      HIP_TRY(hipMemcpyAsync(ctx->d_in, ctx->h_in, sizeof(double) * nin, hipMemcpyHostToDevice, st));
-      int r = launch(ctx, n_draws, ctx->d_in, ctx->d_in + nb, ctx->d_out, dsite, st,
-                     heig ? ctx->d_in + nb + nm : nullptr);
-      if (r) return r;
-      HIP_TRY(hipMemcpyAsync(ctx->h_out, ctx->d_out, sizeof(double) * no, hipMemcpyDeviceToHost, st));
-      return PHY_OK;
+      return launch_small(ctx, n_draws, nin, nb, nm, no, heig, dsite, st);
     });
     if (rc) return rc;
     if (site_ll)
