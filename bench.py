@@ -56,9 +56,8 @@ def parse():
     ap.add_argument("--wg-budget", type=int, default=0)
     ap.add_argument("--cols", type=int, default=0, help="pattern columns per lane (0 = automatic)")
     ap.add_argument("--lds-budget", type=int, default=0)
-    ap.add_argument("--engine", choices=["auto", "pattern", "class", "resident"], default="auto",
-                    help="pattern sweep, class sweep (site repeats), resident class sweep (per draw-category "
-                         "state in LDS) or the context's automatic choice")
+    ap.add_argument("--engine", choices=["auto", "pattern", "class"], default="auto",
+                    help="pattern sweep, class sweep (site repeats) or the context's automatic choice")
     ap.add_argument("--json-out", default=None)
     ap.add_argument("--shard-of", type=int, default=0,
                     help="evaluate only the first of this many pattern shards on one GPU, with no collective -- "
@@ -77,7 +76,7 @@ def parse():
 
 def kernel_source_hash():
     h = hashlib.sha1()
-    for name in ("phylo_hip.hip", "class_engine.inc", "resident_engine.inc", "quad_engine.inc", "multi_device.inc"):
+    for name in ("phylo_hip.hip", "class_engine.inc", "quad_engine.inc", "multi_device.inc"):
         with open(os.path.join(ROOT, "phylostan_amd", "csrc", name), "rb") as fp:
             h.update(fp.read())
     return h.hexdigest()[:12]
@@ -164,17 +163,6 @@ def class_algorithmic_bytes(C, classes, stage, staged, draws):
     (secondary children) are also stored and read back by the segmented
     reduction -- 2 x 32 B more (a primary child's are reduced in registers)."""
     return 32 * C * (3 * classes + 2 * stage + 2 * staged) * draws
-
-
-def resident_algorithmic_bytes(C, B, root_classes, record_vectors, draws):
-    """HBM bytes of one resident-class-sweep launch pair: per
-    (draw, category) the matrix records are read by both kernels (32 B per
-    vector), ps_c pi.p_root written once per root class and read by every
-    category's reverse (C reads), the B dL/dP rows written (128 B each), the
-    scalar slot; per draw log L per root class.  Moved and upper partials
-    never leave LDS."""
-    per_dc = 2 * 32 * record_vectors + 8 * root_classes * (1 + C) + 128 * B + 64
-    return (C * per_dc + 8 * root_classes) * draws
 
 
 def survey_bytes(S, P, C, draws):
@@ -379,8 +367,6 @@ def main():
     info["engine"] = eng.engine()
     if info["engine"] == "class":
         info.update({"class_" + k: v for k, v in eng.class_info().items()})
-    if info["engine"] == "resident":
-        info.update({"resident_" + k: v for k, v in eng.resident_info().items()})
     B = eng.B
     P_local = sl.p1 - sl.p0
 
@@ -492,8 +478,8 @@ def main():
     # the sampler path (host buffers, compact rows -- what phylostan run
     # issues): µs per call of 4 draws (NUTS, one draw per chain) and the
     # evals/s of ADVI's ELBO estimate, elbo_samples = 100 draws per call
-    # (phylostan.py:47), on the pattern sweep (one kernel launch per call,
-    # DESIGN.md 5) and on the resident class sweep
+    # (phylostan.py:47), on the pattern sweep (its quad form for the 4-draw
+    # call)
     sampler = draws_100 = None
     if batched and rank == 0 and world == 1 and not args.no_sampler_latency:
         from phylostan_amd.engine import TreeLikelihood
@@ -510,19 +496,11 @@ def main():
             lk = TreeLikelihood(prob["tipcodes"], prob["weights"], prob["peel0"], prob["rooted"], prob["model"],
                                 C, max_draws=n, device=local)
             lk.set_output(compact=True)
-            try:
-                lk.set_engine(name)
-            except Exception:  # the resident sweep refuses trees that do not fit (e.g. unrooted DS1)
-                lk.close()
-                return None
+            lk.set_engine(name)
             return lk
 
-        for name in ("pattern", "resident"):
+        for name in ("pattern",):
             lk = sampler_ctx(name, 4)
-            if lk is None:
-                sampler[name + "_us_per_call"] = None
-                draws_100[name] = None
-                continue
             for _ in range(20):
                 lk.evaluate_rows(bl4, mv4)
             ta = time.perf_counter()
@@ -544,10 +522,6 @@ def main():
     if info["engine"] == "class":
         alg = class_algorithmic_bytes(C, info["class_classes"], info["class_stage"], info["class_staged"], draws)
         kernel_name = "class sweep: cls_clade_fwd/cls_fwd/cls_root/cls_red/cls_fix_list/cls_rev/cls_clade_rev kernels, forward through reverse"
-    elif info["engine"] == "resident":
-        alg = resident_algorithmic_bytes(C, B, info["resident_root_classes"], info["resident_record_vectors"],
-                                         draws)
-        kernel_name = "resident class sweep: res_fwd_kernel + res_rev_kernel"
     else:
         alg = algorithmic_bytes(S, P_local, C, info["nslots"] - info.get("recomputed", 0), B, draws)
         kernel_name = "sweep_kernel"

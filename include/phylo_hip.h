@@ -228,15 +228,13 @@ int phy_set_output(phy_ctx* ctx, int compact);
  * (site repeats: the forward pass once per distinct tip-state tuple of each
  * subtree, the reverse on upper partials aggregated per tuple -- the exact,
  * total form of the reference's column-reuse cache, pruner/tree.cpp:140-174),
- * 3 = resident class sweep (the class sweep with each (draw, category)'s
- * whole class state in LDS, one workgroup per (draw, category); rooted trees
- * whose state fits in 160 KiB only, else PHY_EINVAL; measured slower than
- * the pattern sweep on fluA / HCV, so never chosen automatically),
  * 0 = automatic (class sweep for alignments of >= 16384 patterns whose
  * subtree classes are at most a quarter of the pattern sweep's node-pattern
  * work).  Results agree to rounding either way.  PHY_ENGINE sets the default
- * at phy_create.  phy_engine returns the engine the next launch uses (0
- * pattern, 1 class, 2 resident). */
+ * at phy_create.  Mode 3 (round 3's resident class sweep) is retired and
+ * refused with PHY_EINVAL: the quad sweep is faster for a sampler's calls on
+ * every workload.  phy_engine returns the engine the next launch uses (0
+ * pattern, 1 class). */
 int phy_set_engine(phy_ctx* ctx, int mode);
 int phy_engine(const phy_ctx* ctx);
 
@@ -257,13 +255,6 @@ int phy_class_info(const phy_ctx* ctx, long long* classes, int* levels, int* roo
  * 1024 classes); PHY_CLADE=k at phy_create fixes k levels (0: off).
  * Results are bitwise the same either way. */
 int phy_class_clades(const phy_ctx* ctx, int* fused_levels, int* clades, long long* largest);
-
-/* Resident class sweep plan (engine 3; zeros when none is built): LDS bytes
- * of one (draw, category) workgroup, non-root classes, levels, root classes,
- * reverse chunks of 16 classes (their dL/dP partials are summed in LDS) and
- * matrix-record vectors staged per (draw, category). */
-int phy_resident_info(const phy_ctx* ctx, int* lds_bytes, long long* classes, int* levels, int* root_classes,
-                      int* partials, int* record_vectors);
 
 #ifdef __cplusplus
 }

@@ -58,8 +58,6 @@ SIGNATURES = {
                                       ctypes.POINTER(ctypes.c_longlong), ctypes.POINTER(ctypes.c_longlong),
                                       _c_int_p, _c_int_p]),
     "phy_class_clades": (ctypes.c_int, [ctypes.c_void_p, _c_int_p, _c_int_p, ctypes.POINTER(ctypes.c_longlong)]),
-    "phy_resident_info": (ctypes.c_int, [ctypes.c_void_p, _c_int_p, ctypes.POINTER(ctypes.c_longlong), _c_int_p,
-                                         _c_int_p, _c_int_p, _c_int_p]),
 }
 
 

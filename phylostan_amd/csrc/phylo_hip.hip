@@ -2109,8 +2109,6 @@ __global__ void __launch_bounds__(QFIN_THREADS) qfin_kernel(QfinArgs qa) {
 namespace {
 struct ClassEngine;  // class_engine.inc
 void free_class_engine(ClassEngine* e);
-struct ResEngine;  // resident_engine.inc
-void free_res_engine(ResEngine* e);
 struct MultiState;  // multi_device.inc
 void free_multi(MultiState* m);
 }  // namespace
@@ -2143,14 +2141,12 @@ struct phy_ctx {
   bool recompute = true;       // rebuild cherries in the reverse instead of storing them
   bool fin_pref = true;        // finalize inside the sweep when one workgroup runs a draw (PHY_FIN=0: off)
   int nrec = 0;                // cherries recomputed under the current plan
-  // engine: 0 = pattern sweep (sweep_kernel), 1 = class sweep (site repeats,
-  // class_engine.inc), 2 = resident class sweep (resident_engine.inc);
-  // engine_pref 0 = automatic, 1 = pattern, 2 = class, 3 = resident
+  // engine: 0 = pattern sweep (sweep_kernel; the quad sweep for small
+  // calls), 1 = class sweep (site repeats, class_engine.inc);
+  // engine_pref 0 = automatic, 1 = pattern, 2 = class
   int engine = 0, engine_pref = 0;
   ClassEngine* ce = nullptr;
-  ResEngine* re = nullptr;
   MultiState* ms = nullptr;  // a multi-device context (phy_create_multi): its shards do the work
-  bool re_tried = false;       // the resident plan was built (or found not to apply)
   int compact = 0;             // output rows without the dL/dP block (phy_set_output)
   double* d_grows = nullptr;   // dL/dP rows when compact: [max_draws][16 C B]
   std::vector<uint8_t> h_tips;  // host copies of the static data (the class plan is built on demand)
@@ -2227,7 +2223,6 @@ void free_ctx(phy_ctx* c) {
   for (hipEvent_t e : c->ev) (void)hipEventDestroy(e);
   for (auto& g : c->graphs) (void)hipGraphExecDestroy(g.ex);
   free_class_engine(c->ce);
-  free_res_engine(c->re);
   free_multi(c->ms);
   if (c->stream) (void)hipStreamDestroy(c->stream);
   (void)hipSetDevice(dev_old);
@@ -2425,7 +2420,6 @@ int dalloc(T** p, size_t n) {
 
 constexpr size_t LDS_CAP = 160 * 1024;
 
-#include "resident_engine.inc"
 constexpr int PIN_DRAWS = 128;  // phy_eval batches up to this size go through pinned staging
                                 // (ADVI's elbo_samples = 100 fits: phylostan.py:47)
 #ifndef PHY_DIRECT_OUT_DEFAULT
@@ -2613,25 +2607,10 @@ int ensure_class_plan(phy_ctx* c) {
                             c->vec_of, c->R, c->nmat, c->gpos, &c->ce);
 }
 
-int ensure_res_plan(phy_ctx* c) {
-  if (c->re_tried) return PHY_OK;
-  c->re_tried = true;
-  return build_res_engine(c->S, c->P, c->C, c->rooted, c->h_tips.data(), c->h_w.data(), c->h_peel.data(),
-                          c->vec_of, c->R, c->nmat, c->gpos, LDS_CAP, &c->re);
-}
-
 int select_engine(phy_ctx* c) {
   ++c->plan_gen;
   c->engine = 0;
   if (c->engine_pref == 1) return PHY_OK;
-  if (c->engine_pref == 3) {
-    int rc = ensure_res_plan(c);
-    if (rc) return rc;
-    if (!c->re) return fail(PHY_EINVAL, "resident class sweep: needs a rooted tree whose per-(draw, category) "
-                                        "class state fits in LDS");
-    c->engine = 2;
-    return PHY_OK;
-  }
   if (c->engine_pref == 0 && c->P < 16384) return PHY_OK;
   int rc = ensure_class_plan(c);
   if (rc) return rc;
@@ -2759,35 +2738,6 @@ bool launch_finalize(FinArgs fa, int n, hipStream_t st) {
   return fa.qf != 0;
 }
 
-// The resident class sweep (resident_engine.inc): forward + root L, then the
-// forward again with the reverse, one workgroup per (draw, category) each
-// (the reverse writes the dL/dP rows itself); the shared finalize.  The
-// timed region spans the two sweep kernels.
-int launch_res(phy_ctx* ctx, int n, const double* d_blens, const double* d_model, double* d_out,
-               double* d_site, hipStream_t st, double* grows, long long gstride, bool* qdone) {
-  ResEngine* e = ctx->re;
-  const int C = ctx->C, B = ctx->B;
-  int rc = res_engine_reserve(e, n);
-  if (rc) return rc;
-  const ResArgs a = res_args(e, ctx->d_pmat, d_model, ctx->extra, grows, gstride);
-  const int dcn = n * C;
-  hipEvent_t e0 = nullptr, e1 = nullptr;
-  if (ctx->timing && (rc = timing_begin(ctx, st, &e0, &e1))) return rc;
-  hipLaunchKernelGGL(res_fwd_kernel, dim3(dcn), dim3(RES_THREADS), e->lds, st, a);
-  hipLaunchKernelGGL(res_rev_kernel, dim3(dcn), dim3(RES_THREADS), e->lds, st, a);
-  HIP_TRY(hipGetLastError());
-  if (ctx->timing) HIP_TRY(hipEventRecord(e1, st));
-  if (d_site)
-    hipLaunchKernelGGL(cls_site_kernel, dim3((ctx->P + 255) / 256, n), dim3(256), 0, st,
-                       (const double*)e->d_sitecls, (const int*)e->d_pat_root, d_site, ctx->P, e->nroot);
-  FinArgs fa{ctx->d_gslot, e->d_sslot, ctx->d_pmat, ctx->eig_cur, d_blens, d_model, ctx->d_gpos, ctx->d_inner, d_out,
-             C,            B,          ctx->nmat,   1,           phy_output_len(ctx), 0, ctx->R, grows, gstride,
-             ctx->kind,    0,          ctx->qfuse_pref ? 1 : 0};
-  *qdone = launch_finalize(fa, n, st);
-  HIP_TRY(hipGetLastError());
-  return PHY_OK;
-}
-
 int launch(phy_ctx* ctx, int n, const double* d_blens, const double* d_model, double* d_out,
            double* d_site, hipStream_t st, const double* d_eig_in = nullptr) {
   const int C = ctx->C, B = ctx->B;
@@ -2818,9 +2768,8 @@ int launch(phy_ctx* ctx, int n, const double* d_blens, const double* d_model, do
   // the chain rule runs inside the sweep (one workgroup per draw) or the
   // finalize kernel unless PHY_QFUSE=0
   bool qdone = false;
-  int rc0 = ctx->engine == 1   ? launch_class(ctx, n, d_blens, d_model, d_out, d_site, st, grows, gstride, &qdone)
-            : ctx->engine == 2 ? launch_res(ctx, n, d_blens, d_model, d_out, d_site, st, grows, gstride, &qdone)
-                               : launch_pattern(ctx, n, d_blens, d_model, d_out, d_site, st, grows, gstride, &qdone);
+  int rc0 = ctx->engine == 1 ? launch_class(ctx, n, d_blens, d_model, d_out, d_site, st, grows, gstride, &qdone)
+                             : launch_pattern(ctx, n, d_blens, d_model, d_out, d_site, st, grows, gstride, &qdone);
   if (rc0) return rc0;
   if (!qdone) {
     FinArgs qa{ctx->d_gslot, ctx->d_sslot, ctx->d_pmat, ctx->eig_cur, d_blens, d_model, ctx->d_gpos, ctx->d_inner,
@@ -2839,7 +2788,7 @@ int launch(phy_ctx* ctx, int n, const double* d_blens, const double* d_model, do
 // GPU-side gaps between its dependent kernels, which a graph keeps, not by
 // host launch cost): the first run of an operand set
 // (draw count, buffers, stream) is direct -- it makes any lazy allocation
-// (class / resident reserves) -- the second is captured and instantiated,
+// (class reserves) -- the second is captured and instantiated,
 // later ones replay it: one graph launch instead of up to ~50 kernel
 // launches (the class sweep's levels).  Engine reserves are grown before
 // the lookup; growth or any replan bumps plan_gen, and stale graphs are
@@ -2853,9 +2802,6 @@ int launch_graphed(phy_ctx* ctx, int n, const void* bl, const void* md, const vo
     int rc = PHY_OK;
     if (ctx->engine == 1 && n > ctx->ce->max_draws) {
       if ((rc = class_engine_reserve(ctx->ce, n, st))) return rc;
-      ++ctx->plan_gen;
-    } else if (ctx->engine == 2 && n > ctx->re->max_draws) {
-      if ((rc = res_engine_reserve(ctx->re, n))) return rc;
       ++ctx->plan_gen;
     }
   }
@@ -3208,8 +3154,6 @@ int phy_create(int S, int P, int C, int rooted, int model, const uint8_t* tipcod
     for (int k = 0; k < 8; ++k)
       (void)hipFuncSetAttribute(sweep_kernel_ptr(1 + (k & 1), (k >> 1) & 1, (k >> 2) & 1),
                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)LDS_CAP);
-    (void)hipFuncSetAttribute((const void*)res_fwd_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)LDS_CAP);
-    (void)hipFuncSetAttribute((const void*)res_rev_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)LDS_CAP);
     (void)hipFuncSetAttribute((const void*)finalize_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)LDS_CAP);
     for (const void* kern : {(const void*)qsweep_kernel<256>, (const void*)qsweep_kernel<1024>}) {
       hipFuncAttributes fa{};  // its static eigensystem copy counts against the cap too
@@ -3718,8 +3662,10 @@ int phy_set_engine(phy_ctx* ctx, int mode) {
     }
     return PHY_OK;
   }
-  if (mode < 0 || mode > 3)
-    return fail(PHY_EINVAL, "engine must be 0 (automatic), 1 (pattern), 2 (class) or 3 (resident)");
+  if (mode == 3)
+    return fail(PHY_EINVAL, "engine 3 (the resident class sweep) was retired: the quad sweep is faster for a "
+                            "sampler's calls on every workload (DESIGN.md 5d)");
+  if (mode < 0 || mode > 2) return fail(PHY_EINVAL, "engine must be 0 (automatic), 1 (pattern) or 2 (class)");
   HIP_TRY(hipSetDevice(ctx->device));
   HIP_TRY(hipStreamSynchronize(ctx->stream));
   ctx->engine_pref = mode;
@@ -3755,20 +3701,6 @@ int phy_class_clades(const phy_ctx* ctx, int* fused_levels, int* clades, long lo
   if (fused_levels) *fused_levels = e ? e->Lc : 0;
   if (clades) *clades = e ? e->nclade : 0;
   if (largest) *largest = e ? e->clade_max : 0;
-  return PHY_OK;
-}
-
-int phy_resident_info(const phy_ctx* ctx, int* lds_bytes, long long* classes, int* levels, int* root_classes,
-                      int* partials, int* record_vectors) {
-  if (!ctx) return fail(PHY_EINVAL, "NULL ctx");
-  if (ctx->ms) return phy_resident_info(ctx->ms->shard[0], lds_bytes, classes, levels, root_classes, partials, record_vectors);
-  const ResEngine* e = ctx->re;
-  if (lds_bytes) *lds_bytes = e ? (int)e->lds : 0;
-  if (classes) *classes = e ? e->classes : 0;
-  if (levels) *levels = e ? e->L : 0;
-  if (root_classes) *root_classes = e ? e->nroot : 0;
-  if (partials) *partials = e ? e->nchunks : 0;
-  if (record_vectors) *record_vectors = e ? e->nmc : 0;
   return PHY_OK;
 }
 

@@ -265,42 +265,37 @@ class TreeLikelihood:
         self._st = None  # the staging rows follow the row length
 
     def set_engine(self, mode=0):
-        """0 automatic, 1 pattern sweep, 2 class sweep (site repeats), 3 resident
-        class sweep (the class sweep with each draw-category's state in LDS)."""
+        """0 automatic, 1 pattern sweep (its quad form for calls of <= 16
+        draws), 2 class sweep (site repeats).  Round 3's resident class sweep
+        (mode 3) is retired: phy_set_engine refuses it."""
         if isinstance(mode, str):
-            mode = {"auto": 0, "pattern": 1, "class": 2, "resident": 3}[mode]
+            mode = {"auto": 0, "pattern": 1, "class": 2}[mode]
         _lib.check(self.lib.phy_set_engine(self.ctx, int(mode)), "phy_set_engine")
 
     def prefer_latency_engine(self, probe=True, calls=24):
         """For host-driven samplers (a few draws per call, one call per
-        leapfrog / ELBO round): the faster of the pattern sweep (the quad
-        sweep for <= 16 draws) and the resident class sweep (when the tree is
-        rooted and its class state fits in LDS), measured here: ``calls``
-        synchronous calls of ``max_draws`` synthetic draws (branch lengths
-        0.05, uniform frequencies, unit rates) on each, in two alternating
-        rounds, the lower median kept.  One box, 4 draws (r04g/h): fluA quad
-        112 against resident 137 us per call, HCV 106 against 97 -- neither
-        wins everywhere, so it is measured, not guessed.  The choice affects
-        speed only: both engines pass the same parity tests (results agree to
-        the parity tolerances, not bitwise).  probe=False: the resident sweep
-        when it applies (round 3's rule).  Without the resident sweep: the
-        automatic engine.  Returns the name; the timings (us per call) are in
+        leapfrog / ELBO round): the pattern sweep (its quad form for <= 16
+        draws) -- faster than round 3's resident class sweep on every
+        workload (fluA 99.8 against 132 us per 4-draw call) -- unless the
+        automatic choice is the class sweep (a large alignment); then both are
+        measured here (``calls`` synchronous calls of ``max_draws`` synthetic
+        draws -- branch lengths 0.05, uniform frequencies, unit rates -- on
+        each, in two alternating rounds, the lower median kept) and the
+        faster is kept.  The choice affects speed only: both engines pass the
+        same parity tests.  probe=False: the automatic engine's choice.
+        Returns the name; timings (us per call), when measured, are in
         ``self.latency_probe``."""
-        try:
-            self.set_engine("resident")
-        except _lib.PhyloHipError:
-            self.set_engine("auto")
-            return self.engine()
-        if not probe:
+        self.set_engine("auto")
+        if self.engine() == "pattern" or not probe:
             return self.engine()
         import time
         n = self.max_draws
         bl = np.full((n, self.B), 0.05)
         mv = np.repeat(self.model_vector([0.25] * 4, [1.0] * 6, [1.0] * self.C, [1.0 / self.C] * self.C)[None], n,
                        axis=0)
-        times = {"pattern": [], "resident": []}
+        times = {"pattern": [], "class": []}
         for rnd in range(2):
-            for name in ("pattern", "resident"):
+            for name in ("pattern", "class"):
                 self.set_engine(name)
                 for _ in range(3):
                     self.evaluate_rows(bl, mv)
@@ -314,8 +309,8 @@ class TreeLikelihood:
         return self.engine()
 
     def engine(self):
-        """The engine the next launch uses: "pattern", "class" or "resident"."""
-        return ("pattern", "class", "resident")[self.lib.phy_engine(self.ctx)]
+        """The engine the next launch uses: "pattern" or "class"."""
+        return ("pattern", "class")[self.lib.phy_engine(self.ctx)]
 
     def class_info(self):
         ll = [ctypes.c_longlong() for _ in range(3)]
@@ -329,16 +324,6 @@ class TreeLikelihood:
         return dict(classes=ll[0].value, levels=ii[0].value, root_classes=ii[1].value, stage=ll[1].value,
                     staged=ll[2].value, tiles=ii[2].value, spans=ii[3].value, clade_levels=fl.value,
                     clades=nc.value, clade_max=big.value)
-
-    def resident_info(self):
-        """The resident class sweep's plan (zeros when it has none)."""
-        ii = [ctypes.c_int() for _ in range(5)]
-        cl = ctypes.c_longlong()
-        _lib.check(self.lib.phy_resident_info(self.ctx, ctypes.byref(ii[0]), ctypes.byref(cl), ctypes.byref(ii[1]),
-                                              ctypes.byref(ii[2]), ctypes.byref(ii[3]), ctypes.byref(ii[4])),
-                   "phy_resident_info")
-        return dict(lds_bytes=ii[0].value, classes=cl.value, levels=ii[1].value, root_classes=ii[2].value,
-                    partials=ii[3].value, record_vectors=ii[4].value)
 
     def timing_start(self):
         _lib.check(self.lib.phy_timing_start(self.ctx), "phy_timing_start")

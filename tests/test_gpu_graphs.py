@@ -28,7 +28,7 @@ def _inputs(case, n, seed):
     return bl, mv
 
 
-@pytest.mark.parametrize("engine", ["pattern", "class", "resident"])
+@pytest.mark.parametrize("engine", ["pattern", "class"])
 def test_graph_replay_host_path(engine):
     case = cases.fluA_case()
     a, b = _pair(case, 8)

@@ -165,8 +165,8 @@ def test_batched_draws_match_single(wg_budget):
 
 
 @pytest.mark.parametrize("make,engine", [(cases.fluA_case, "pattern"), (cases.hcv_case, "pattern"),
-                                         (cases.fluA_case, "resident"), (cases.hcv_case, "class")],
-                         ids=["fluA-pattern", "HCV-pattern", "fluA-resident", "HCV-class"])
+                                         (cases.fluA_case, "class"), (cases.hcv_case, "class")],
+                         ids=["fluA-pattern", "HCV-pattern", "fluA-class", "HCV-class"])
 def test_production_batch_every_row_vs_c_port(make, engine):
     """The bench's shape: 1,024 distinct parameter draws in ONE launch (the
     pattern sweep then runs one workgroup per draw with the finalize fused),
@@ -423,7 +423,7 @@ def test_tuning_grows_workgroup_regions_past_create():
 
 
 
-@pytest.mark.parametrize("engine", ["pattern", "class", "resident"])
+@pytest.mark.parametrize("engine", ["pattern", "class"])
 @pytest.mark.parametrize("S,rooted,max_draws", [(3, True, 1), (3, False, 1), (4, False, 1), (3, True, 4096),
                                                 (3, False, 4096)],
                          ids=["S3-rooted", "S3-unrooted", "S4-unrooted", "S3-rooted-batched", "S3-unrooted-batched"])
@@ -431,15 +431,13 @@ def test_minimal_trees(engine, S, rooted, max_draws):
     """The smallest trees the boundary accepts (S = 3; an unrooted tree's root
     then has a tip child on the merged branch), on every engine, with the
     sampler's one-column plan (max_draws 1) and the batched two-column plan."""
-    if engine == "resident" and not rooted:
-        pytest.skip("the resident sweep takes rooted trees only (test_resident_refuses_unrooted)")
     case = cases.random_case(31 + S, S=S, P=7, C=2, model="GTR", rooted=rooted)
     eng = _engine(case, max_draws=max_draws)
     eng.set_engine(engine)
     check_case(case, eng)
 
 
-@pytest.mark.parametrize("engine", ["pattern", "class", "resident"])
+@pytest.mark.parametrize("engine", ["pattern", "class"])
 def test_zero_and_saturated_branches_and_zero_weights(engine):
     """Internal branch lengths of zero (P = I, dP/dt = Q; a zero tip branch
     would make patterns impossible) and branches of 40 substitutions (P at
@@ -456,7 +454,7 @@ def test_zero_and_saturated_branches_and_zero_weights(engine):
     check_case(case, eng)
 
 
-@pytest.mark.parametrize("engine", ["pattern", "class", "resident"])
+@pytest.mark.parametrize("engine", ["pattern", "class"])
 @pytest.mark.parametrize("max_draws", [8, 4096], ids=["one-column", "batched"])
 def test_impossible_draw_inside_a_batch(engine, max_draws):
     """One draw of a batch with L = 0 (mixture weights all zero) comes back
@@ -475,3 +473,14 @@ def test_impossible_draw_inside_a_batch(engine, max_draws):
         one = eng.evaluate_rows(bl[k:k + 1], mv[k:k + 1])[0]
         assert np.array_equal(rows[k], one), k
         assert np.isfinite(rows[k]).all()
+
+
+def test_retired_resident_engine_is_refused():
+    """Engine 3 (round 3's resident class sweep) is retired: phy_set_engine
+    refuses it with PHY_EINVAL and a message naming the replacement."""
+    from phylostan_amd._lib import PhyloHipError
+    case = cases.fluA_case()
+    eng = _engine(case, max_draws=4)
+    with pytest.raises(PhyloHipError, match="retired"):
+        eng.set_engine(3)
+    assert eng.engine() == "pattern"

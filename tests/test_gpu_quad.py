@@ -114,20 +114,31 @@ def test_quad_impossible_draw_is_minus_inf(monkeypatch):
     assert np.array_equal(rows[0], good[0]) and np.array_equal(rows[2], good[2])
 
 
-def test_prefer_latency_engine_measures_and_keeps_the_faster(monkeypatch):
-    """prefer_latency_engine times the pattern (quad) and resident sweeps on
-    synthetic draws and keeps the faster; the kept engine's rows agree with
-    the column sweeps'."""
+def test_prefer_latency_engine_is_the_quad_sweep_on_small_alignments(monkeypatch):
+    """prefer_latency_engine keeps the pattern engine (its quad form for the
+    sampler's 4-draw calls) when the automatic choice is the pattern sweep;
+    its rows agree with the column sweep's."""
     case = cases.fluA_case()
     n = 4
     bl, mv = _draws(case, n, 21)
     eng = _engine(case, max_draws=n, monkeypatch=monkeypatch)
-    name = eng.prefer_latency_engine()
-    assert set(eng.latency_probe) == {"pattern", "resident"}
-    assert name == min(eng.latency_probe, key=eng.latency_probe.get)
-    assert all(0.0 < t < 1e5 for t in eng.latency_probe.values())
+    assert eng.prefer_latency_engine() == "pattern"
     rows = eng.evaluate_rows(bl, mv)
     ref = _engine(case, max_draws=n, quad=False, monkeypatch=monkeypatch).evaluate_rows(bl, mv)
     for k in range(n):
         assert abs(rows[k, 0] - ref[k, 0]) <= RTOL_LL * abs(ref[k, 0])
         _close(rows[k, 1:], ref[k, 1:], RTOL_G, "row %d" % k)
+
+
+def test_prefer_latency_engine_measures_class_against_pattern():
+    """On an alignment the automatic choice sends to the class sweep, both
+    engines are timed and the faster kept."""
+    from phylostan_amd import synthetic
+    from phylostan_amd.engine import TreeLikelihood
+    pd, _ = synthetic.simulate(n_sites=60_000)  # the synthetic workload's tree and model, 60k sites
+    eng = TreeLikelihood(pd.tipcodes, pd.weights, pd.peel0, True, "GTR", 4, max_draws=4)
+    eng.set_engine("auto")
+    assert eng.engine() == "class"
+    name = eng.prefer_latency_engine(calls=8)
+    assert set(eng.latency_probe) == {"pattern", "class"}
+    assert name == min(eng.latency_probe, key=eng.latency_probe.get)

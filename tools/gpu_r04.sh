@@ -51,15 +51,13 @@ if want prof; then
   timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof_fluA -o run -- \
     python bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-sampler-latency > $O/prof_fluA.log 2>&1
 fi
-if want lat; then  # small calls: quad sweep against the column sweeps (PHY_QUAD=0) and the resident sweep
+if want lat; then  # small calls: quad sweep against the column sweeps (PHY_QUAD=0)
   for w in fluA HCV DS1; do
     for d in 1 4 16 32; do
       for q in 1 0; do
         PHY_QUAD=$q timeout -k 10 120 python tools/latency_probe.py --workload $w --draws $d --engine pattern \
           > $O/lat_${w}_${d}_q$q.log 2>&1 && tail -1 $O/lat_${w}_${d}_q$q.log | sed "s/^/$w d=$d quad=$q /"
       done
-      timeout -k 10 120 python tools/latency_probe.py --workload $w --draws $d --engine resident \
-        > $O/lat_${w}_${d}_res.log 2>&1 && tail -1 $O/lat_${w}_${d}_res.log | sed "s/^/$w d=$d resident /" || true
     done
   done
   timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof_lat4 -o run -- \

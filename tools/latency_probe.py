@@ -19,7 +19,7 @@ def main():
     ap.add_argument("--draws", type=int, default=4)
     ap.add_argument("--calls", type=int, default=300)
     ap.add_argument("--workload", default="fluA", choices=["fluA", "HCV", "DS1"])
-    ap.add_argument("--engine", default="auto", choices=["auto", "pattern", "class", "resident"])
+    ap.add_argument("--engine", default="auto", choices=["auto", "pattern", "class"])
     ap.add_argument("--cols", type=int, default=0, help="pattern columns per lane (0 = the plan's choice)")
     ap.add_argument("--lds-budget", type=int, default=0)
     a = ap.parse_args()

@@ -17,7 +17,7 @@ sys.path.insert(0, ROOT)
 def main():
     from phylostan_amd.engine import TreeLikelihood
     from tests import cases
-    eng = sys.argv[1] if len(sys.argv) > 1 else "resident"
+    eng = sys.argv[1] if len(sys.argv) > 1 else "pattern"
     n = int(sys.argv[2]) if len(sys.argv) > 2 else 2
     case = cases.fluA_case()
     liks = []

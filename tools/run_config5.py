@@ -28,8 +28,8 @@ def main():
     ap.add_argument("--warmup", type=int, default=1000)
     ap.add_argument("--samples", type=int, default=1000)
     ap.add_argument("--seed", type=int, default=1)
-    ap.add_argument("--engine", default="latency", choices=["latency", "auto", "pattern", "resident"],
-                    help="latency: the resident class sweep when it applies (what the CLI uses for NUTS)")
+    ap.add_argument("--engine", default="latency", choices=["latency", "auto", "pattern"],
+                    help="latency: TreeLikelihood.prefer_latency_engine() (what the CLI uses for NUTS)")
     ap.add_argument("--out", default=os.path.join(ROOT, "gpurun_out", "config5"))
     a = ap.parse_args()
     os.makedirs(a.out, exist_ok=True)
