@@ -2123,6 +2123,7 @@ struct phy_ctx {
   int K = 1;                   // columns per lane of the current plan
   bool klat = false;           // K = 1 latency plan (sweep_kernel<512, 1, .>: no register spills)
   bool klat_pref = true;       // PHY_KLAT=0: the latency plan keeps the four-wave K = 1 kernel
+  bool eig_fuse_pref = true;   // PHY_EIG_FUSE=0: small device batches take eig_kernel + pmat_kernel<false>
   // the quad sweep (quad_engine.inc) for calls of <= QUAD_MAX_DRAWS draws
   bool quad_pref = true;       // PHY_QUAD=0: off
   bool quad_ok = false;        // its LDS plan fits
@@ -2748,7 +2749,7 @@ int launch(phy_ctx* ctx, int n, const double* d_blens, const double* d_model, do
     // eigensystems: given (host-formed, the small host-buffer path); small
     // device batches: each pmat wave forms its draw's (one launch less);
     // large ones: one thread per draw first
-    const int with_eig = (!d_eig_in && n <= EIG_FUSE_MAX) ? 1 : 0;
+    const int with_eig = (!d_eig_in && n <= EIG_FUSE_MAX && ctx->eig_fuse_pref) ? 1 : 0;
     PmatArgs pa{d_model, d_blens, ctx->d_mat_branch, const_cast<double*>(ctx->eig_cur), ctx->d_pmat, C, B, ctx->kind,
                 ctx->nmat, n, ctx->R, ctx->extra, with_eig};
     if (!with_eig && !d_eig_in) {
@@ -3131,6 +3132,7 @@ int phy_create(int S, int P, int C, int rooted, int model, const uint8_t* tipcod
     c->graph_pref = gk ? atoi(gk) != 0 : false;
     const char* lk = getenv("PHY_KLAT");
     c->klat_pref = lk ? atoi(lk) != 0 : true;
+    c->eig_fuse_pref = env_flag("PHY_EIG_FUSE", 1);
     const char* qk2 = getenv("PHY_QUAD");
     c->quad_pref = qk2 ? atoi(qk2) != 0 : true;
 
