@@ -486,6 +486,12 @@ struct Chain {
 struct Sampler {
   int n, dim;
   std::vector<Chain> chains;
+  // phn_run's round state: the pending positions and their chains, and the
+  // round's work arrays
+  bool started = false;
+  int m = 0;
+  Vec Q, Q2, bl, mv, rows, lp, G;
+  std::vector<int> idx, idx2, sel;
 };
 
 }  // namespace
@@ -555,6 +561,55 @@ int phn_step(void* h, int n_in, const int* idx_in, const double* lp_in, const do
     }
   }
   return m;
+}
+
+// The whole sampling loop natively: each gradient round maps the pending
+// positions through the strict-clock posterior's native pre phase
+// (host_model.cpp phh_strict_pre), evaluates the draws that reach the
+// likelihood through `submit` / `wait` (the HIP library's phy_eval_submit /
+// phy_eval_wait on its context `lik`, or any functions of that shape), maps
+// the rows back through phh_strict_post and advances the chains -- what
+// nuts.py's run_chains does through Posterior.log_prob_grad, without a
+// Python round trip per round.  Runs at most max_rounds rounds per call
+// (the caller reports progress between calls).  Returns 1 while chains
+// remain, 0 when all are finished, -(1 + chain) when a chain failed
+// (phn_error), -(1000000 + rc) when submit / wait returned rc != 0.
+typedef int (*phn_submit_t)(void* ctx, int n, const double* blens, const double* model);
+typedef int (*phn_wait_t)(void* ctx, double* out);
+}  // extern "C"
+extern "C" int phh_strict_pre(void* hnd, int n, const double* U, double* blens, double* mv, int* sel);
+extern "C" void phh_strict_post(void* hnd, int n, const double* U, const double* rows, int rowlen, const int* sel,
+                                int need_grad, double* lp, double* G);
+extern "C" {
+
+int phn_run(void* h, void* post, void* lik, phn_submit_t submit, phn_wait_t wait, int B, int ml, int rowlen,
+            int max_rounds, long* rounds) {
+  Sampler* s = (Sampler*)h;
+  const int n = s->n, dim = s->dim;
+  if (!s->started) {
+    s->Q.assign((size_t)n * dim, 0.0), s->Q2 = s->Q, s->G = s->Q;
+    s->bl.assign((size_t)n * B, 0.0), s->mv.assign((size_t)n * ml, 0.0), s->rows.assign((size_t)n * rowlen, 0.0);
+    s->lp.assign(n, 0.0), s->idx.assign(n, 0), s->idx2.assign(n, 0), s->sel.assign(n, 0);
+    s->m = phn_step(h, 0, nullptr, nullptr, nullptr, s->Q.data(), s->idx.data());
+    s->started = true;
+  }
+  for (int r = 0; r < max_rounds && s->m > 0; ++r) {
+    const int m = s->m;
+    const int cnt = phh_strict_pre(post, m, s->Q.data(), s->bl.data(), s->mv.data(), s->sel.data());
+    if (cnt > 0) {
+      int rc = submit(lik, cnt, s->bl.data(), s->mv.data());
+      if (!rc) rc = wait(lik, s->rows.data());
+      if (rc) return -(1000000 + rc);
+    }
+    phh_strict_post(post, m, s->Q.data(), s->rows.data(), rowlen, s->sel.data(), 1, s->lp.data(), s->G.data());
+    const int m2 = phn_step(h, m, s->idx.data(), s->lp.data(), s->G.data(), s->Q2.data(), s->idx2.data());
+    if (m2 < 0) return m2;
+    std::swap(s->Q, s->Q2);
+    std::swap(s->idx, s->idx2);
+    s->m = m2;
+    if (rounds) ++*rounds;
+  }
+  return s->m > 0 ? 1 : 0;
 }
 
 // chain c's failure: 1 non-finite initial log density, 2 step size > 1e7,

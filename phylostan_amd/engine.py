@@ -196,6 +196,16 @@ class TreeLikelihood:
         _lib.check(self.lib.phy_eval_submit(self.ctx, n, pbl, pmv), "phy_eval_submit")
         self._pending = n
 
+    def native_submit_wait(self, n):
+        """(context, phy_eval_submit, phy_eval_wait addresses, row length)
+        for a native caller that evaluates up to n draws per call through the
+        submit / wait pair (nuts.py's native sampling loop), or None when n
+        exceeds what one submit takes."""
+        if n > min(self.max_draws, self._STAGE_DRAWS) or getattr(self, "ctx", None) is None:
+            return None
+        return (self.ctx.value, ctypes.cast(self.lib.phy_eval_submit, ctypes.c_void_p).value,
+                ctypes.cast(self.lib.phy_eval_wait, ctypes.c_void_p).value, self.outlen)
+
     def wait_rows(self):
         """The rows [n, outlen] of the evaluation ``submit_rows`` started."""
         n, self._pending = self._pending, 0

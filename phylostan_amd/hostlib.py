@@ -61,6 +61,10 @@ def load():
             lib.phn_info.restype = ctypes.c_int
             lib.phn_draws.argtypes = [ctypes.c_void_p, _i, _D, _D]
             lib.phn_draws.restype = None
+        if hasattr(lib, "phn_run"):
+            _p = ctypes.c_void_p
+            lib.phn_run.argtypes = [_p, _p, _p, _p, _p, _i, _i, _i, _i, ctypes.POINTER(ctypes.c_long)]
+            lib.phn_run.restype = ctypes.c_int
         _lib = lib
     return _lib
 

@@ -407,23 +407,22 @@ def _run_native(lib, posterior, q0s, seeds, num_warmup, num_samples, thin, progr
                        float(o["stepsize"]), int(o["init_buffer"]), int(o["term_buffer"]), int(o["base_window"]),
                        float(o["max_delta_h"]))
     try:
-        # the round's arrays, addresses resolved once (ndarray.ctypes ~2.5 us)
-        Q, LP, GR = np.empty((n, dim)), np.empty(n), np.empty((n, dim))
-        idx_a, idx_b = np.empty(n, np.int32), np.empty(n, np.int32)
-        pQ, pLP, pGR = Q.ctypes.data, LP.ctypes.data, GR.ctypes.data
-        pa, pb = idx_a.ctypes.data, idx_b.ctypes.data
-        m = lib.phn_step(h, 0, None, None, None, pQ, pa)
-        rounds, t0 = 0, time.time()
-        while m > 0:
-            lp, G = posterior.log_prob_grad(Q[:m])
-            LP[:m] = lp
-            GR[:m] = G
-            pa, pb = pb, pa
-            m = lib.phn_step(h, m, pb, pLP, pGR, pQ, pa)
-            rounds += 1
-            if progress and rounds % 2000 == 0:
-                nd = lib.phn_info(h, 0, None, None, None)
-                progress("NUTS: %d gradient rounds, %d draws (chain 0), %.1f s" % (rounds, nd, time.time() - t0))
+        native_loop = _native_loop_args(posterior, n)
+        if native_loop is not None:  # every round in C++ (phn_run)
+            rounds, t0 = ctypes.c_long(0), time.time()
+            while True:
+                r = lib.phn_run(h, *native_loop, 2000, ctypes.byref(rounds))
+                if r <= 0:
+                    break
+                if progress:
+                    nd = lib.phn_info(h, 0, None, None, None)
+                    progress("NUTS: %d gradient rounds, %d draws (chain 0), %.1f s" % (rounds.value, nd, time.time() - t0))
+            if r <= -1000000:
+                from . import _lib
+                _lib.check(-(r + 1000000), "phy_eval_submit / phy_eval_wait (native NUTS loop)")
+            m = r
+        else:
+            m = _python_rounds(lib, h, posterior, n, dim, progress)
         if m < 0:
             code = lib.phn_error(h, -m - 1)
             raise RuntimeError({1: "NUTS: initial point has non-finite log density",
@@ -442,6 +441,51 @@ def _run_native(lib, posterior, q0s, seeds, num_warmup, num_samples, thin, progr
         return out
     finally:
         lib.phn_free(h)
+
+
+def _native_loop_args(posterior, n):
+    """phn_run's arguments after the sampler handle when the whole round can
+    run natively -- the posterior's strict-clock native phases
+    (hostlib.StrictPosterior) around a TreeLikelihood context whose
+    phy_eval_submit takes all chains at once (n <= max_draws, n <= 128) --
+    else None (the rounds go through Posterior.log_prob_grad).
+    ``PHYLO_NUTS_LOOP=python`` forces the latter."""
+    fast, lik = getattr(posterior, "_fast", None), getattr(posterior, "lik", None)
+    if os.environ.get("PHYLO_NUTS_LOOP") == "python" or fast is None or lik is None:
+        return None
+    native = getattr(lik, "native_submit_wait", None)
+    if native is None:
+        return None
+    sw = native(n)
+    if sw is None:
+        return None
+    ctx, submit, wait, rowlen = sw
+    return (ctypes.c_void_p(fast.h), ctypes.c_void_p(ctx), ctypes.c_void_p(submit), ctypes.c_void_p(wait),
+            fast.B, fast.ml, rowlen)
+
+
+def _python_rounds(lib, h, posterior, n, dim, progress):
+    """The rounds through Posterior.log_prob_grad (any posterior and
+    likelihood): one phn_step per round.  Returns phn_step's last result
+    (0, or -(1 + chain) on a chain failure)."""
+    # the round's arrays, addresses resolved once (ndarray.ctypes ~2.5 us)
+    Q, LP, GR = np.empty((n, dim)), np.empty(n), np.empty((n, dim))
+    idx_a, idx_b = np.empty(n, np.int32), np.empty(n, np.int32)
+    pQ, pLP, pGR = Q.ctypes.data, LP.ctypes.data, GR.ctypes.data
+    pa, pb = idx_a.ctypes.data, idx_b.ctypes.data
+    m = lib.phn_step(h, 0, None, None, None, pQ, pa)
+    rounds, t0 = 0, time.time()
+    while m > 0:
+        lp, G = posterior.log_prob_grad(Q[:m])
+        LP[:m] = lp
+        GR[:m] = G
+        pa, pb = pb, pa
+        m = lib.phn_step(h, m, pb, pLP, pGR, pQ, pa)
+        rounds += 1
+        if progress and rounds % 2000 == 0:
+            nd = lib.phn_info(h, 0, None, None, None)
+            progress("NUTS: %d gradient rounds, %d draws (chain 0), %.1f s" % (rounds, nd, time.time() - t0))
+    return m
 
 
 def run_chains(posterior, q0s, seeds, num_warmup=1000, num_samples=1000, thin=1, progress=None,

@@ -3,7 +3,10 @@ generator chains, their specification: the same seeds give bitwise the same
 draws, statistics, gradient counts, step sizes and metrics (dimensions below
 16, where numpy's dot is one fused multiply-add chain and the native dot
 follows it), through warmup windows, divergences, out-of-support positions,
-thinning and short warmups; longer vectors agree to rounding."""
+thinning and short warmups; longer vectors agree to rounding.  And the
+whole sampling loop in C++ (phn_run: the posterior's native phases, the
+likelihood's submit / wait and the chains) against the same chains driven
+round by round through Posterior.log_prob_grad."""
 import numpy as np
 import pytest
 
@@ -120,3 +123,89 @@ def test_native_chains_improper_posterior():
     for native in (False, True):
         with pytest.raises(RuntimeError, match="improper"):
             nuts.run_chains(Flat(), [np.zeros(2)], [1], num_warmup=10, num_samples=10, native=native)
+
+
+class _RowsLik:
+    """A stand-in likelihood in the TreeLikelihood row layout (log L and
+    d/dblens of a Gaussian in the branch lengths, zero Q-parameter
+    gradients), reachable both ways: evaluate_rows / submit_rows / wait_rows
+    (the Python rounds) and native_submit_wait (C callbacks for phn_run)."""
+
+    def __init__(self, B, C):
+        import ctypes
+        self.B, self.C = B, C
+        self.outlen = 1 + B + 2 * C + 14
+        self.calls = 0
+        self._pending = None
+        SUB = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p)
+        WAIT = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p)
+
+        def sub(ctx, n, bl, mv):
+            self._pending = np.ctypeslib.as_array(ctypes.cast(bl, ctypes.POINTER(ctypes.c_double)),
+                                                  shape=(n, self.B)).copy()
+            return 0
+
+        def wait(ctx, out):
+            rows = self.evaluate_rows(self._pending, None)
+            dst = np.ctypeslib.as_array(ctypes.cast(out, ctypes.POINTER(ctypes.c_double)), shape=rows.shape)
+            dst[...] = rows
+            return 0
+
+        self._cb = (SUB(sub), WAIT(wait))  # alive while the sampler runs
+
+    def evaluate_rows(self, blens, mv):
+        self.calls += 1
+        x = np.asarray(blens) - 0.02
+        rows = np.zeros((x.shape[0], self.outlen))
+        rows[:, 0] = -0.5 * 2e3 * (x * x).sum(1)
+        rows[:, 1:1 + self.B] = -2e3 * x
+        return rows
+
+    def submit_rows(self, blens, mv):
+        self._pending = np.array(blens)
+
+    def wait_rows(self):
+        return self.evaluate_rows(self._pending, None)
+
+    def native_submit_wait(self, n):
+        import ctypes
+        return (0, ctypes.cast(self._cb[0], ctypes.c_void_p).value, ctypes.cast(self._cb[1], ctypes.c_void_p).value,
+                self.outlen)
+
+
+def _strict_posterior(lik_factory):
+    from phylostan_amd.posterior import ModelSpec, Posterior, TreeData
+    from tests import cases
+    d = cases.load_layout("fluA")
+    S = d["tipbits"].shape[0]
+    tree = TreeData(S, d["peel"] - 1, d["map"], d["lowers"], float(d["oldest"]))
+    spec = ModelSpec(model="HKY", categories=4, clock="strict", estimate_rate=True, coalescent="constant",
+                     heterochronous=True)
+    lik = lik_factory(2 * S - 2, 4)
+    post = Posterior(spec, tree, lik, compact_rows=True)
+    if post._fast is None:
+        pytest.skip("the strict-clock posterior's native phases are not built")
+    return post, lik
+
+
+def test_native_loop_equals_python_rounds(monkeypatch):
+    """phn_run (pre, likelihood callbacks, post and the chains all in C++)
+    gives the draws of the same native chains driven round by round through
+    Posterior.log_prob_grad, bit for bit, on the strict-clock fluA posterior
+    with a stand-in likelihood; and it made no Python likelihood round trip
+    of its own beyond the callbacks."""
+    post_a, lik_a = _strict_posterior(_RowsLik)
+    post_b, lik_b = _strict_posterior(_RowsLik)
+    q0s = [post_a.initial_point(np.random.default_rng((1, c))) for c in range(4)]
+    kw = dict(num_warmup=60, num_samples=40, native=True)
+    monkeypatch.setenv("PHYLO_NUTS_LOOP", "python")
+    a = nuts.run_chains(post_a, q0s, [(1, c) for c in range(4)], **kw)
+    monkeypatch.delenv("PHYLO_NUTS_LOOP")
+    assert nuts._native_loop_args(post_b, 4) is not None
+    b = nuts.run_chains(post_b, q0s, [(1, c) for c in range(4)], **kw)
+    assert lik_a.calls == lik_b.calls > 0
+    for ca, cb in zip(a, b):
+        assert ca.n_grad == cb.n_grad and ca.eps == cb.eps
+        for da, db in zip(ca.draws, cb.draws):
+            np.testing.assert_array_equal(da[0], db[0])
+            assert da[1:] == db[1:]
