@@ -104,6 +104,32 @@ def test_fluA_nuts_short_multichain():
         assert np.all(np.isfinite(lps)) and lps[-1] > lp0[c]
 
 
+def test_fluA_native_nuts_loop_equals_python_rounds(monkeypatch):
+    """The whole NUTS loop in C++ (phn_run: the posterior's native phases
+    and phy_eval_submit / phy_eval_wait called from the sampler) gives the
+    draws of the same native chains driven round by round from Python
+    through Posterior.log_prob_grad -- bit for bit, on the GPU."""
+    from phylostan_amd import nuts
+    from phylostan_amd.engine import TreeLikelihood
+    runs = []
+    for mode in ("python", None):
+        if mode:
+            monkeypatch.setenv("PHYLO_NUTS_LOOP", mode)
+        else:
+            monkeypatch.delenv("PHYLO_NUTS_LOOP", raising=False)
+        post, d = _fluA_posterior(TreeLikelihood, max_draws=4)
+        if mode is None:
+            assert nuts._native_loop_args(post, 4) is not None
+        q0s = [post.initial_point(np.random.default_rng((3, c))) for c in range(4)]
+        runs.append(nuts.run_chains(post, q0s, [(3, c) for c in range(4)], num_warmup=30, num_samples=10,
+                                    max_depth=6))
+    for ca, cb in zip(*runs):
+        assert ca.n_grad == cb.n_grad and ca.eps == cb.eps
+        for da, db in zip(ca.draws, cb.draws):
+            np.testing.assert_array_equal(da[0], db[0])
+            assert da[1:] == db[1:]
+
+
 def test_fluA_fullrank_advi_runs_to_convergence(tmp_path):
     """-q fullrank (phylostan.py:311-313 algorithm='fullrank') on fluA with
     eta fixed at 0.1 (phylostan run --eta 0.1: no adaptation; the value the
