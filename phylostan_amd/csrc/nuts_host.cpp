@@ -81,7 +81,7 @@ bool criterion(const Vec& ps_minus, const Vec& ps_plus, const Vec& rho) {  // nu
 
 struct Chain {
   // waits: the chain has asked for (lp, grad) at q_eval
-  enum State { W_INIT, W_ISS_FIRST, W_ISS_LOOP, W_LEAF, DONE, FAILED };
+  enum State { W_INIT, W_ISS_FIRST, W_ISS_LOOP, W_LEAF, W_HMC, DONE, FAILED };
   enum Cont { AFTER_INIT, AFTER_WINDOW };
 
   int dim;
@@ -120,6 +120,12 @@ struct Chain {
   double t_accept, t_energy;
   int t_depth, t_nlf;
   bool t_div;
+  // static HMC (nuts.py StaticHMCChain: Stan's adapt_diag_e_static_hmc)
+  bool hmc = false;
+  double T = 0.0;  // integration time
+  long L = 1;      // leapfrog steps
+  long hk = 0;     // steps taken in this transition
+  Point z_init;
   // the pending evaluation
   Point* ev;
   double ev_eps;
@@ -378,13 +384,41 @@ struct Chain {
     t_energy = H(z_sample);
   }
 
+  // ---------------------------------------------------- static HMC
+  void update_L() {  // nuts.py StaticHMCChain._update_L: L = max(1, int(T / eps))
+    const double r = T / eps;
+    L = r >= 1.0 ? (r < 2147483647.0 ? (long)r : 2147483647L) : 1;
+  }
+
+  void hmc_start() {  // StaticHMCChain._transition up to its first leapfrog
+    z_sample = z;
+    z_sample.p = sample_p();
+    z_init = z_sample;
+    H0 = H(z_sample);
+    n_lf = (int)L;
+    hk = 0;
+    evolve_begin(z_sample, eps);
+    state = W_HMC;
+  }
+
+  void hmc_finish() {
+    double h = H(z_sample);
+    if (std::isnan(h)) h = INFINITY;
+    const double acc = h == INFINITY ? 0.0 : (H0 - h > 0 ? 1.0 : std::exp(H0 - h));
+    if (acc < 1.0 && uniform() > acc) z_sample = z_init;
+    t_accept = (acc < 1.0) ? acc : 1.0;  // Python's min(1.0, accept)
+    t_nlf = n_lf;
+    t_div = false;
+    t_energy = H(z_sample);
+  }
+
   // ------------------------------------------------------------ program
   void iter_finish() {
     if (warm && it == num_warmup - 1) eps = std::exp(x_bar);  // complete_adaptation
     if (it % thin == 0) {
       dq.insert(dq.end(), z.q.begin(), z.q.end());
-      double st[8] = {z.lp, t_accept, eps_used, (double)t_depth, (double)t_nlf, t_div ? 1.0 : 0.0, t_energy,
-                      warm ? 1.0 : 0.0};
+      double st[8] = {z.lp, t_accept, eps_used, hmc ? T : (double)t_depth, (double)t_nlf, t_div ? 1.0 : 0.0,
+                      t_energy, warm ? 1.0 : 0.0};
       dstat.insert(dstat.end(), st, st + 8);
     }
     ++it;
@@ -396,6 +430,10 @@ struct Chain {
     while (it < total) {
       warm = it < num_warmup;
       eps_used = eps;
+      if (hmc) {
+        hmc_start();
+        return true;
+      }
       tr_start();
       if (tr_depth()) return true;
       tr_finish();
@@ -413,8 +451,10 @@ struct Chain {
     z = std::move(a);
     if (warm) {
       learn_stepsize(t_accept);
+      if (hmc) update_L();
       if (learn_variance(z.q)) {
         if (iss_start(AFTER_WINDOW)) return true;
+        if (hmc) update_L();
         da_restart();
       }
     }
@@ -450,6 +490,7 @@ struct Chain {
         } else {
           bool stop = (idir == 1 && !(dH > l08)) || (idir == -1 && !(dH < l08));
           if (stop) {
+            if (cont == AFTER_WINDOW && hmc) update_L();  // (not after the initial one: nuts.py's order)
             da_restart();
             if (cont == AFTER_INIT) {
               it = 0;
@@ -464,6 +505,16 @@ struct Chain {
         }
         iss_loop();
         return true;
+      }
+      case W_HMC: {
+        evolve_end(lp, g);
+        if (++hk < n_lf) {
+          evolve_begin(z_sample, eps);
+          return true;
+        }
+        hmc_finish();
+        if (after_transition()) return true;
+        return run_iterations();
       }
       case W_LEAF: {
         evolve_end(lp, g);
@@ -532,6 +583,18 @@ void* phn_create(int nchains, int dim, const double* q0, void* const* bitgens, i
 }
 
 void phn_free(void* h) { delete (Sampler*)h; }
+
+// Every chain a static HMC chain instead (nuts.py StaticHMCChain: a fixed
+// integration time T over L = max(1, int(T / eps)) leapfrog steps, one
+// Metropolis accept of the end point; the draw record carries T in the
+// tree-depth slot); call before the first phn_step.
+void phn_set_static_hmc(void* h, double int_time) {
+  for (Chain& ch : ((Sampler*)h)->chains) {
+    ch.hmc = true;
+    ch.T = int_time;
+    ch.update_L();
+  }
+}
 
 // One gradient round.  n_in chains (idx_in) hand back (lp_in[k], G_in[k]) for
 // the positions the previous call asked for (n_in = 0 on the first call:

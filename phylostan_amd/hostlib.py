@@ -61,6 +61,9 @@ def load():
             lib.phn_info.restype = ctypes.c_int
             lib.phn_draws.argtypes = [ctypes.c_void_p, _i, _D, _D]
             lib.phn_draws.restype = None
+        if hasattr(lib, "phn_set_static_hmc"):
+            lib.phn_set_static_hmc.argtypes = [ctypes.c_void_p, ctypes.c_double]
+            lib.phn_set_static_hmc.restype = None
         if hasattr(lib, "phn_run"):
             _p = ctypes.c_void_p
             lib.phn_run.argtypes = [_p, _p, _p, _p, _p, _i, _i, _i, _i, ctypes.POINTER(ctypes.c_long)]

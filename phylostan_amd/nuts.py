@@ -389,14 +389,16 @@ def native_available():
     return lib if lib is not None and hasattr(lib, "phn_create") else None
 
 
-def _run_native(lib, posterior, q0s, seeds, num_warmup, num_samples, thin, progress, max_depth, **kw):
-    """``Chain`` programs run by csrc/nuts_host.cpp (the same algorithm and
-    random streams; tests/test_nuts_native.py): one C call per gradient
-    round advances every chain and returns the positions of the next
-    batched ``posterior.log_prob_grad`` call."""
+def _run_native(lib, posterior, q0s, seeds, num_warmup, num_samples, thin, progress, max_depth, hmc=False, **kw):
+    """``Chain`` (or, hmc=True, ``StaticHMCChain``) programs run by
+    csrc/nuts_host.cpp (the same algorithm and random streams;
+    tests/test_nuts_native.py): one C call per gradient round advances every
+    chain and returns the positions of the next batched
+    ``posterior.log_prob_grad`` call."""
+    int_time = float(kw.pop("int_time", 2 * math.pi)) if hmc else None
     bad = set(kw) - set(_CHAIN_OPTIONS)
     if bad:
-        raise TypeError("unexpected NUTS option(s) %s" % sorted(bad))
+        raise TypeError("unexpected %s option(s) %s" % ("HMC" if hmc else "NUTS", sorted(bad)))
     o = dict(_CHAIN_OPTIONS, **kw)
     dim, n = posterior.dim, len(q0s)
     rngs = [np.random.default_rng(sd) for sd in seeds]  # alive while the chains draw from them
@@ -406,6 +408,8 @@ def _run_native(lib, posterior, q0s, seeds, num_warmup, num_samples, thin, progr
                        int(max_depth), float(o["delta"]), float(o["gamma"]), float(o["kappa"]), float(o["t0"]),
                        float(o["stepsize"]), int(o["init_buffer"]), int(o["term_buffer"]), int(o["base_window"]),
                        float(o["max_delta_h"]))
+    if hmc:
+        lib.phn_set_static_hmc(h, int_time)
     try:
         native_loop = _native_loop_args(posterior, n)
         if native_loop is not None:  # every round in C++ (phn_run)
@@ -425,7 +429,7 @@ def _run_native(lib, posterior, q0s, seeds, num_warmup, num_samples, thin, progr
             m = _python_rounds(lib, h, posterior, n, dim, progress)
         if m < 0:
             code = lib.phn_error(h, -m - 1)
-            raise RuntimeError({1: "NUTS: initial point has non-finite log density",
+            raise RuntimeError({1: "%s: initial point has non-finite log density" % ("HMC" if hmc else "NUTS"),
                                 2: "NUTS: posterior is improper (step size > 1e7)",
                                 3: "NUTS: no acceptable small step size"}.get(code, "NUTS: chain failed (%d)" % code))
         out = []
@@ -435,7 +439,8 @@ def _run_native(lib, posterior, q0s, seeds, num_warmup, num_samples, thin, progr
             nd = lib.phn_info(h, c, ctypes.byref(ng), ctypes.byref(eps), im.ctypes.data)
             q, st = np.empty((nd, dim)), np.empty((nd, 8))
             lib.phn_draws(h, c, q.ctypes.data, st.ctypes.data)
-            draws = [(q[k], float(s[0]), float(s[1]), float(s[2]), int(s[3]), int(s[4]), int(s[5]), float(s[6]),
+            slot3 = float if hmc else int  # HMC: the integration time in the tree-depth slot
+            draws = [(q[k], float(s[0]), float(s[1]), float(s[2]), slot3(s[3]), int(s[4]), int(s[5]), float(s[6]),
                       bool(s[7])) for k, s in enumerate(st)]
             out.append(NativeChain(dim, draws, int(ng.value), float(eps.value), im))
         return out
@@ -503,11 +508,16 @@ def run_chains(posterior, q0s, seeds, num_warmup=1000, num_samples=1000, thin=1,
     dim = posterior.dim
     if native is None:
         native = os.environ.get("PHYLO_NUTS", "native") != "python"
-    lib = native_available() if native and algorithm != "hmc" else None
-    if native and algorithm != "hmc" and lib is None and os.environ.get("PHYLO_NUTS") == "native":
-        raise RuntimeError("PHYLO_NUTS=native but libphylo_host.so has no NUTS chains (run build())")
+    lib = native_available() if native else None
+    if lib is not None and algorithm == "hmc" and not hasattr(lib, "phn_set_static_hmc"):
+        lib = None
+    if native and lib is None and os.environ.get("PHYLO_NUTS") == "native":
+        raise RuntimeError("PHYLO_NUTS=native but libphylo_host.so has no native chains (run build())")
     if lib is not None:
-        return _run_native(lib, posterior, q0s, seeds, num_warmup, num_samples, thin, progress, max_depth, **kw)
+        if algorithm == "hmc":
+            kw.pop("max_depth", None)
+        return _run_native(lib, posterior, q0s, seeds, num_warmup, num_samples, thin, progress, max_depth,
+                           hmc=algorithm == "hmc", **kw)
     if algorithm == "hmc":
         chains = [StaticHMCChain(dim, q0, np.random.default_rng(sd), num_warmup, num_samples, thin, **kw)
                   for q0, sd in zip(q0s, seeds)]

@@ -209,3 +209,29 @@ def test_native_loop_equals_python_rounds(monkeypatch):
         for da, db in zip(ca.draws, cb.draws):
             np.testing.assert_array_equal(da[0], db[0])
             assert da[1:] == db[1:]
+
+
+@pytest.mark.parametrize("name,tgt,kw", [
+    ("1d", Gauss([2.0]), dict(num_warmup=200, num_samples=200)),
+    ("3d", Gauss([1.0, 2.0, 0.5]), dict(num_warmup=150, num_samples=60)),
+    ("rejections", Gauss([1.0, 0.5], trunc=-1.5), dict(num_warmup=100, num_samples=60)),
+    ("short-thin", Gauss([1.0, 2.0]), dict(num_warmup=15, num_samples=20, thin=3, int_time=1.0)),
+    ("options", Gauss([1.0, 2.0]), dict(num_warmup=120, num_samples=30, delta=0.9, stepsize=0.3, int_time=3.0)),
+])
+def test_native_static_hmc_bitwise_equal_to_generators(name, tgt, kw):
+    """Static HMC (nuts.py StaticHMCChain, Stan's adapt_diag_e_static_hmc) on
+    the native chains: the same draws, with the integration time in the
+    tree-depth slot as a float."""
+    q0s = [np.full(tgt.dim, 0.3 * k) for k in range(3)]
+    seeds = [(5, k) for k in range(3)]
+    a = nuts.run_chains(tgt, q0s, seeds, native=False, algorithm="hmc", **kw)
+    b = nuts.run_chains(tgt, q0s, seeds, native=True, algorithm="hmc", **kw)
+    _assert_same(a, b)
+    assert isinstance(b[0].draws[0][4], float)
+
+
+def test_native_static_hmc_errors_match():
+    tgt = Gauss([1.0, 1.0], trunc=0.5)
+    for native in (False, True):
+        with pytest.raises(RuntimeError, match="HMC: initial point has non-finite log density"):
+            nuts.run_chains(tgt, [np.zeros(2)], [1], num_warmup=10, num_samples=10, native=native, algorithm="hmc")
