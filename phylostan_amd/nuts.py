@@ -16,6 +16,12 @@ log density and gradient it needs; ``run_chains`` advances all chains in
 lockstep and evaluates the pending positions of all of them in ONE batched
 call (one GPU launch of ``n_chains`` draws), so 8 chains cost about as much
 wall time per leapfrog step as one.
+
+The generators below are the specification.  ``run_chains`` runs the same
+programs natively by default (csrc/nuts_host.cpp: a state machine per chain
+drawing from the chains' numpy Generators, bitwise these chains' draws up to
+15 dimensions), and for the strict-clock posterior around a TreeLikelihood
+the whole round loop too (``phn_run``: no Python per gradient round).
 """
 import ctypes
 import math
