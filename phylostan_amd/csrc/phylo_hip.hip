@@ -2669,7 +2669,7 @@ int launch_class(phy_ctx* ctx, int n, const double* d_blens, const double* d_mod
     if (!L.nchunk) continue;
     a.first = L.chunk0;
     a.count = L.nchunk;
-    hipLaunchKernelGGL(cls_fwd_kernel, dim3((L.nchunk + 3) / 4, dcn), dim3(256), 0, st, a);
+    hipLaunchKernelGGL(cls_fwd_kernel, dim3((L.nchunk + CLS_WPG - 1) / CLS_WPG, dcn), dim3(CLS_THREADS), 0, st, a);
   }
   {
     auto rk = C <= 4 ? (e->root_tips ? cls_root_kernel<256, true> : cls_root_kernel<256, false>)
@@ -2681,23 +2681,23 @@ int launch_class(phy_ctx* ctx, int n, const double* d_blens, const double* d_mod
     if (L.ntile) {
       a.first = L.tile0;
       a.count = L.ntile;
-      hipLaunchKernelGGL(cls_red_kernel, dim3((L.ntile + 3) / 4, dcn), dim3(256), 0, st, a);
+      hipLaunchKernelGGL(cls_red_kernel, dim3((L.ntile + CLS_WPG - 1) / CLS_WPG, dcn), dim3(CLS_THREADS), 0, st, a);
     }
     if (L.nlfix)  // the level's long spans (the short ones are summed by the REV lanes)
-      hipLaunchKernelGGL(cls_fix_list_kernel, dim3((L.nlfix + 3) / 4, dcn), dim3(256), 0, st, a,
+      hipLaunchKernelGGL(cls_fix_list_kernel, dim3((L.nlfix + CLS_WPG - 1) / CLS_WPG, dcn), dim3(CLS_THREADS), 0, st, a,
                          (const int*)e->d_lfix + L.lfix0, L.nlfix);
     if (L.nchunk) {
       a.first = L.chunk0;
       a.count = L.nchunk;
-      hipLaunchKernelGGL(cls_rev_kernel, dim3((L.nchunk + 3) / 4, dcn), dim3(256), 0, st, a);
+      hipLaunchKernelGGL(cls_rev_kernel, dim3((L.nchunk + CLS_WPG - 1) / CLS_WPG, dcn), dim3(CLS_THREADS), 0, st, a);
     }
   }
   if (e->Lc > 0) {
     if (e->nrtile)
-      hipLaunchKernelGGL(cls_red_list_kernel, dim3((e->nrtile + 3) / 4, dcn), dim3(256), 0, st, a,
+      hipLaunchKernelGGL(cls_red_list_kernel, dim3((e->nrtile + CLS_WPG - 1) / CLS_WPG, dcn), dim3(CLS_THREADS), 0, st, a,
                          (const int*)e->d_rtile, e->nrtile);
     if (e->nrspan)
-      hipLaunchKernelGGL(cls_fix_list_kernel, dim3((e->nrspan + 3) / 4, dcn), dim3(256), 0, st, a,
+      hipLaunchKernelGGL(cls_fix_list_kernel, dim3((e->nrspan + CLS_WPG - 1) / CLS_WPG, dcn), dim3(CLS_THREADS), 0, st, a,
                          (const int*)e->d_rspan, e->nrspan);
     hipLaunchKernelGGL(cls_clade_rev_kernel, dim3(e->nclade, dcn), dim3(CLADE_THREADS), 0, st, a,
                        (const CladeLevel*)e->d_clade, e->Lc);
