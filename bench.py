@@ -68,6 +68,17 @@ def parse():
                          "devices 0..N-1, one RCCL all-reduce of the output rows inside the C-ABI, or a device-side "
                          "sum when the box has fewer GPUs than shards -- the reference boundary's single handle, "
                          "eigen/prune_stan.hpp:9-17); parallelism multidevN")
+    ap.add_argument("--no-synthetic", action="store_true",
+                    help="skip the synthetic 128 x 1M sub-record of the default (fluA) run")
+    ap.add_argument("--synthetic-steps", type=int, default=None,
+                    help="timed steps of the synthetic sub-record (default: --steps, at least 20)")
+    ap.add_argument("--synthetic-draws", type=int, default=1,
+                    help="parameter points per step of the synthetic sub-record")
+    ap.add_argument("--no-multidev", action="store_true",
+                    help="skip the phy_create_multi leg of the synthetic sub-record under --gpus N > 1")
+    ap.add_argument("--rehearse", action="store_true",
+                    help="N > 1 rehearsal on a one-GPU box: every rank on device 0, gloo instead of RCCL for the "
+                         "collectives (the line says so); checks the multi-rank path, measures nothing")
     ap.add_argument("--dry-run", action="store_true",
                     help="launcher check only: ranks join a gloo group on the CPU, all-reduce their rank "
                          "ids and exit (no GPU, no evaluation)")
@@ -133,8 +144,9 @@ def synthetic_problem(sites):
         pd, prm = synthetic.simulate(n_sites=sites)
         d = dict(tipcodes=pd.tipcodes, weights=pd.weights, peel0=pd.peel0, **prm)
         try:
-            np.savez(cache + ".tmp.npz", **d)
-            os.replace(cache + ".tmp.npz", cache)
+            tmp = "%s.%d.tmp.npz" % (cache, os.getpid())  # ranks may simulate side by side
+            np.savez(tmp, **d)
+            os.replace(tmp, cache)
         except OSError:
             pass
     return dict(tipcodes=d["tipcodes"], weights=d["weights"], peel0=d["peel0"], rooted=True,
@@ -276,6 +288,224 @@ def parameter_sets(prob, nuniq, draws, B, C, rng):
     return blens, mvs
 
 
+TORCHRUN_ENV = ("RANK", "LOCAL_RANK", "WORLD_SIZE", "LOCAL_WORLD_SIZE", "GROUP_RANK", "GROUP_WORLD_SIZE",
+                "ROLE_RANK", "ROLE_WORLD_SIZE", "ROLE_NAME", "MASTER_ADDR", "MASTER_PORT", "TORCHELASTIC_RUN_ID",
+                "TORCHELASTIC_RESTART_COUNT", "TORCHELASTIC_MAX_RESTARTS", "TORCHELASTIC_USE_AGENT_STORE",
+                "TORCH_NCCL_ASYNC_ERROR_HANDLING", "TORCHELASTIC_ERROR_FILE")
+
+
+def multidev_child(n, steps, warmup, sites, draws, timeout=300):
+    """The in-boundary multi-device leg: ``bench.py --workload synthetic
+    --multi-device n`` as a child process (one process, ONE phy_create_multi
+    handle over devices 0..n-1, one ncclAllReduce of the output rows per
+    evaluation inside the C-ABI -- eigen/prune_stan.hpp:9-17's single
+    synchronous handle).  A child, with its own time limit, so a failure of
+    that path is reported in the line instead of taking the run down."""
+    import subprocess
+    import tempfile
+    env = {k: v for k, v in os.environ.items() if k not in TORCHRUN_ENV}
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    fd, path = tempfile.mkstemp(prefix="phylo_multidev_", suffix=".json")
+    os.close(fd)
+    cmd = [sys.executable, os.path.abspath(__file__), "--workload", "synthetic", "--multi-device", str(n),
+           "--steps", str(steps), "--warmup", str(warmup), "--sites", str(sites), "--draws", str(draws),
+           "--no-cpu-baseline", "--json-out", path]
+    t0 = time.perf_counter()
+    try:
+        cp = subprocess.run(cmd, env=env, timeout=timeout, stdout=subprocess.PIPE, stderr=subprocess.PIPE)
+        with open(path) as fp:
+            txt = fp.read().strip()
+        if cp.returncode != 0 or not txt:
+            return dict(ok=False, returncode=cp.returncode, stderr_tail=cp.stderr.decode(errors="replace")[-600:])
+        sub = json.loads(txt.splitlines()[-1])
+        keep = ("value", "unit", "n_gpus", "ms_per_step", "steps", "warmup", "nominal_loglik")
+        out = {k: sub.get(k) for k in keep}
+        out["devices"] = sub["config"].get("devices")
+        out["reduction"] = sub["config"].get("reduction")
+        out["roofline_kernel_avg_ms"] = sub["roofline"]["kernel_avg_ms"]
+        out.update(ok=True, wall_s=time.perf_counter() - t0, command=" ".join(cmd[1:-2]))
+        return out
+    except subprocess.TimeoutExpired:
+        return dict(ok=False, error="timed out after %d s" % timeout)
+    except (OSError, ValueError, KeyError) as e:
+        return dict(ok=False, error=repr(e))
+    finally:
+        try:
+            os.unlink(path)
+        except OSError:
+            pass
+
+
+def synthetic_leg(args, world, rank, local, dev, cpu_group):
+    """BASELINE.json config 4 inside the default run: the synthetic 128-taxon x
+    1M-site GTR+W4 workload, ``--synthetic-draws``
+    parameter points per step, its patterns sharded over the run's ranks
+    (contiguous whole 128-pattern blocks) with ONE all-reduce(SUM) of the
+    fp64 output rows per step over RCCL inside the timed
+    region.  At N = 1 it is the one-GPU evaluation (no collective).  Returns
+    the sub-record for rank 0's JSON line (None elsewhere)."""
+    import torch
+    import torch.distributed as dist
+    from phylostan_amd.distributed import ShardedLikelihood
+
+    t_setup = time.perf_counter()
+    prob = synthetic_problem(args.sites)
+    S, P = prob["tipcodes"].shape
+    C = prob["C"]
+    draws = max(1, args.synthetic_draws)
+    sl = ShardedLikelihood(prob["tipcodes"], prob["weights"], prob["peel0"], prob["rooted"], prob["model"], C,
+                           rank, world, device=local, max_draws=draws)
+    eng = sl.engine
+    info = {"engine": eng.engine()}
+    if info["engine"] == "class":
+        info.update({"class_" + k: v for k, v in eng.class_info().items()})
+    B = eng.B
+    rng = np.random.default_rng(4321 + rank)
+    steps = args.synthetic_steps or max(20, args.steps)
+    warm = max(3, min(args.warmup, 10))
+    nuniq = min(steps + warm, 8)
+    blens, mvs = parameter_sets(prob, nuniq, draws, B, C, rng)
+    d_blens = torch.tensor(blens, device=dev, dtype=torch.float64)
+    d_model = torch.tensor(mvs, device=dev, dtype=torch.float64)
+    d_out = torch.zeros((draws, eng.outlen), device=dev, dtype=torch.float64)
+    stream = torch.cuda.current_stream(dev).cuda_stream
+    setup_s = time.perf_counter() - t_setup
+
+    def step(k):
+        sl.evaluate(d_blens[k % nuniq], d_model[k % nuniq], d_out, stream=stream)
+
+    def max_over_ranks(x):
+        if world == 1:
+            return x
+        t = torch.tensor([x], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return float(t.item())
+
+    def timed(fn, n):
+        torch.cuda.synchronize(dev)
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        for k in range(n):
+            fn(k)
+        torch.cuda.synchronize(dev)
+        if world > 1:
+            dist.barrier()
+        return max_over_ranks(time.perf_counter() - t0)
+
+    for k in range(warm):
+        step(k)
+    elapsed = timed(lambda k: step(warm + k), steps)
+    # the class sweep's launches (forward through reverse) on HIP events
+    eng.timing_start()
+    for k in range(steps):
+        sl.engine.evaluate_device(d_blens[k % nuniq].data_ptr(), d_model[k % nuniq].data_ptr(), d_out.data_ptr(),
+                                  0, n_draws=draws, stream=stream)
+    torch.cuda.synchronize(dev)
+    kern_ms, nl = eng.timing_read()
+    kern_avg_ms = max_over_ranks(kern_ms / max(nl, 1))
+    allreduce = None
+    if world > 1:  # the step's one collective alone: the full fp64 rows, ~130 KB per draw
+        buf = torch.zeros_like(d_out)
+        for _ in range(5):
+            dist.all_reduce(buf)
+        ar = timed(lambda k: dist.all_reduce(buf), 50)
+        allreduce = dict(us_per_call=1e6 * ar / 50, bytes=buf.numel() * 8, op="all_reduce(SUM) fp64, RCCL")
+    step(0)  # parameter set 0, draw 0: the nominal point
+    torch.cuda.synchronize(dev)
+    row0 = d_out[0].double().cpu().numpy()
+    value = draws * steps / elapsed  # whole-job: every step is one evaluation of the whole alignment
+
+    alg = class_algorithmic_bytes(C, info["class_classes"], info["class_stage"], info["class_staged"], draws) \
+        if info["engine"] == "class" else \
+        algorithmic_bytes(S, sl.p1 - sl.p0, C, eng.program_info()["nslots"], B, draws)
+    achieved = alg / (kern_avg_ms * 1e-3) / 1e9
+    traffic = None
+    if world == 1:
+        traffic = pmc_record("synthetic", draws, info["engine"])
+
+    if world > 1:
+        dist.barrier(group=cpu_group)
+    rec = None
+    if rank == 0:
+        hinfo = host_cpu_info()
+        cpu = None
+        if world == 1 and not args.no_cpu_baseline:
+            # bounded sample: ONE full evaluation of the whole alignment, one thread (~10-20 s)
+            cpu, ref = cpu_baseline(prob, 0.0, info=hinfo)
+        else:  # the check only: the C port on every host thread this job may use
+            from oracle import cpu as ocpu
+            from phylostan_amd import models
+            ref, _ = ocpu.evaluate(prob["tipcodes"], prob["weights"], prob["peel0"], prob["rooted"],
+                                   models.MODEL_IDS[prob["model"]],
+                                   models.model_vector(prob["freqs"], prob["rates"], prob["rs"], prob["ps"]),
+                                   prob["blens"], C, nthreads=hinfo["threads"])
+        rel = abs(row0[0] - ref[0]) / max(abs(ref[0]), 1e-300)
+        g, gr = row0[1:1 + B], ref[1:1 + B]
+        grel = float(np.max(np.abs(g - gr)) / max(np.max(np.abs(gr)), 1e-300))
+        check = dict(gpu_loglik_nominal=float(row0[0]), cpu_loglik_nominal=float(ref[0]), rel_err=rel,
+                     grad_blens_max_rel_err=grel, ok=bool(rel <= 1e-10 and grel <= 1e-8),
+                     reference="oracle/cpu_pruner.c on the whole alignment (all-reduced rows at N > 1)")
+        multidev = None
+        if world > 1 and not args.no_multidev:
+            multidev = multidev_child(world, max(10, steps // 2), 3, args.sites, draws)
+            if multidev.get("ok") and multidev.get("nominal_loglik") is not None:
+                r = abs(multidev["nominal_loglik"] - ref[0]) / abs(ref[0])
+                multidev["nominal_rel_err"] = r
+        rec = {
+            "metric": METRIC["synthetic"],
+            "value": value,
+            "unit": "evals/s",
+            "n_gpus": world,
+            "steps": steps,
+            "warmup": warm,
+            "ms_per_step": 1e3 * elapsed / steps,
+            "higher_is_better": True,
+            "scaling": "strong",
+            "dtype": "f64",
+            "data": DATA["synthetic"],
+            "config": {"workload": "synthetic 128 x %d sites GTR+W4 (BASELINE config 4), %d draw%s per step, "
+                                   "patterns sharded over %d rank%s, one all-reduce of the rows per step"
+                                   % (args.sites, draws, "" if draws == 1 else "s", world,
+                                      "" if world == 1 else "s"),
+                       "taxa": S, "patterns": P, "patterns_per_rank": sl.p1 - sl.p0, "categories": C,
+                       "branches": B, "draws_per_step": draws, "parallelism": "patterns%d" % world},
+            "roofline": {"bound": "hbm", "achieved": achieved, "peak": PEAK_HBM_GBPS, "unit": "GB/s",
+                         "frac": achieved / PEAK_HBM_GBPS, "traffic": traffic, "per": "GPU (rank 0's shard)",
+                         "kernel": "class sweep, forward through reverse (DESIGN.md 5b)" if info["engine"] == "class"
+                         else "sweep_kernel",
+                         "kernel_avg_ms": kern_avg_ms, "algorithmic_bytes_per_launch": alg,
+                         "survey_model_bytes_per_launch": survey_bytes(S, sl.p1 - sl.p0, C, draws),
+                         "limiter": "latency / launch chain: dependent kernels per tree level (DESIGN.md 5b)"},
+            "allreduce": allreduce,
+            "cpu_baseline": cpu,
+            "nominal_check": check,
+            "multidev": multidev,
+            "program": info,
+            "setup_s": setup_s,
+        }
+    if world > 1:
+        dist.barrier(group=cpu_group)
+    eng.close()
+    return rec
+
+
+def pmc_record(workload, draws, engine):
+    """The committed PMC HBM bytes per launch of this kernel source (None when
+    profiles/pmc_traffic.json is of another source or lacks the key)."""
+    pmc = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    try:
+        with open(pmc) as fp:
+            rec = json.load(fp)
+        key = "%s:%d:%s" % (workload, draws, engine)
+        if rec.get("kernel_source") == kernel_source_hash() and key in rec.get("per_launch_bytes", {}):
+            return rec["per_launch_bytes"][key]
+    except (OSError, ValueError):
+        pass
+    return None
+
+
 def main():
     args = parse()
     env_world = os.environ.get("WORLD_SIZE")
@@ -301,9 +531,16 @@ def main():
             print(json.dumps({"dry_run": True, "n_gpus": world, "sum_of_ranks": total}), flush=True)
         return
 
+    cpu_group = None
+    if args.rehearse:
+        local = 0
     if world > 1:
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if args.rehearse:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        cpu_group = dist.new_group(backend="gloo")  # host-side waits (rank 0's CPU work, the multidev child)
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
 
@@ -322,6 +559,8 @@ def main():
                                          prob["model"], C, max_draws=max_draws, devices=self.devices)
             self.p0, self.p1 = 0, prob["tipcodes"].shape[1]
             self.world = 1
+            self.reduction = ("rccl all-reduce (ncclCommInitAll, distinct devices)" if len(set(self.devices)) > 1
+                              else "device-side shard sum (one device)" if n > 1 else "none (one shard)")
 
         def evaluate(self, d_blens, d_model, d_out, stream=None):
             self.engine.evaluate_device(d_blens.data_ptr(), d_model.data_ptr(), d_out.data_ptr(), 0,
@@ -508,6 +747,16 @@ def main():
                 lk.evaluate_rows(bl4, mv4)
             sampler[name + "_us_per_call"] = 1e6 * (time.perf_counter() - ta) / 300
             lk.close()
+            # ADVI's gradient: grad_samples = 1 draw per call (phylostan.py:49), the
+            # reference's commonest call (`phylostan run` defaults to -a vb)
+            lk = sampler_ctx(name, 1)
+            for _ in range(20):
+                lk.evaluate_rows(bl4[:1], mv4[:1])
+            ta = time.perf_counter()
+            for _ in range(300):
+                lk.evaluate_rows(bl4[:1], mv4[:1])
+            sampler[name + "_us_per_call_1draw"] = 1e6 * (time.perf_counter() - ta) / 300
+            lk.close()
             lk = sampler_ctx(name, 100)
             for _ in range(5):
                 lk.evaluate_rows(bl100, mv100)
@@ -526,17 +775,11 @@ def main():
         alg = algorithmic_bytes(S, P_local, C, info["nslots"] - info.get("recomputed", 0), B, draws)
         kernel_name = "sweep_kernel"
     achieved = alg / (kern_avg_ms * 1e-3) / 1e9
+    flops = survey_flops(S, P_local, C, draws)
+    achieved_tf = flops / (kern_avg_ms * 1e-3) / 1e12
     traffic = None
-    pmc = os.path.join(ROOT, "profiles", "pmc_traffic.json")
-    if os.path.exists(pmc) and args.shard_of <= 1:  # the PMC record is of the whole workload, not a shard
-        try:
-            with open(pmc) as fp:
-                rec = json.load(fp)
-            key = "%s:%d:%s" % (args.workload, draws, info["engine"])
-            if rec.get("kernel_source") == kernel_source_hash() and key in rec.get("per_launch_bytes", {}):
-                traffic = rec["per_launch_bytes"][key]
-        except (OSError, ValueError):
-            traffic = None
+    if args.shard_of <= 1 and not args.multi_device:  # the PMC record is of the whole workload, not a shard
+        traffic = pmc_record(args.workload, draws, info["engine"])
 
     # compute side of the same kernel (rocprofv3 SQ counters, tools/pmc_sq.py,
     # same kernel source only): fp64 FLOP rate against the vector peak and
@@ -561,6 +804,41 @@ def main():
                                      "SQ cycle counters in quad-cycles)"}
         except (OSError, ValueError, KeyError):
             compute = None
+
+    if info["engine"] == "pattern":
+        # The pattern sweep keeps p and q on chip (SURVEY.md 8d's byte model, which materialises them,
+        # would put this kernel above the HBM peak), and its counters say fp64 VALU issue / latency
+        # (profiles/sq_counters.json): it is priced against the fp64 vector roof with SURVEY.md 8d's
+        # algorithmic flops, F = 244 C P (S-1) per evaluation; the HBM view is reported beside it.
+        roofline = {
+            "bound": "fp64-vector", "achieved": achieved_tf, "peak": PEAK_FP64_TFLOPS, "unit": "TFLOP/s",
+            "frac": achieved_tf / PEAK_FP64_TFLOPS, "traffic": traffic,
+            "kernel": kernel_name, "kernel_avg_ms": kern_avg_ms,
+            "algorithmic_flops_per_launch": flops,
+            "limiter": "fp64 VALU issue / latency at two waves per SIMD: the SIMDs issue about half of the "
+                       "wave-cycles and wait on s_waitcnt most of the rest (profiles/sq_counters.json); counted "
+                       "HBM traffic is far below the 8 TB/s roof",
+            "hbm": {"achieved": achieved, "peak": PEAK_HBM_GBPS, "unit": "GB/s", "frac": achieved / PEAK_HBM_GBPS,
+                    "algorithmic_bytes_per_launch": alg,
+                    "survey_model_bytes_per_launch": survey_bytes(S, P_local, C, draws),
+                    "traffic_over_algorithmic": (traffic / alg) if traffic else None},
+            "compute": compute,
+        }
+    else:
+        roofline = {
+            "bound": "hbm", "achieved": achieved, "peak": PEAK_HBM_GBPS, "unit": "GB/s",
+            "frac": achieved / PEAK_HBM_GBPS, "traffic": traffic,
+            "kernel": kernel_name, "kernel_avg_ms": kern_avg_ms,
+            "algorithmic_bytes_per_launch": alg,
+            "survey_model_bytes_per_launch": survey_bytes(S, P_local, C, draws),
+            "survey_flops_frac": achieved_tf / PEAK_FP64_TFLOPS,
+            "limiter": "latency / launch chain: one small dependent kernel per tree level (DESIGN.md 5b)",
+        }
+
+    synth = None
+    if args.workload == "fluA" and not args.no_synthetic and args.shard_of <= 1 and not args.multi_device:
+        eng.close()  # the headline's context is done: its memory back before the 1M-site shard's
+        synth = synthetic_leg(args, world, rank, local, dev, cpu_group)
 
     cpu = cpu_mt = check = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:  # the CPU baseline is an N=1 figure
@@ -600,23 +878,7 @@ def main():
                 "devices": sl.devices if args.multi_device else None,
                 "projection_shard_of": args.shard_of or None,
             },
-            "roofline": {
-                "bound": "hbm", "achieved": achieved, "peak": PEAK_HBM_GBPS, "unit": "GB/s",
-                "frac": achieved / PEAK_HBM_GBPS, "traffic": traffic,
-                "kernel": kernel_name, "kernel_avg_ms": kern_avg_ms,
-                "algorithmic_bytes_per_launch": alg,
-                "survey_model_bytes_per_launch": survey_bytes(S, P_local, C, draws),
-                # SURVEY.md 8d's flops per evaluation over the same launch time, against the fp64 vector peak
-                "survey_flops_frac": survey_flops(S, P_local, C, draws) / (kern_avg_ms * 1e-3) / 1e12
-                / PEAK_FP64_TFLOPS,
-                # what actually limits the kernel: the byte roof above is the bound the
-                # contract prices against; the counters say instruction issue / latency
-                "limiter": ("issue/latency: SQ counters show the SIMDs issuing about half of the wave-cycles "
-                            "and waiting on s_waitcnt most of the rest (profiles/sq_counters.json); counted HBM "
-                            "traffic is below the 8 TB/s roof" if info["engine"] == "pattern" else
-                            "latency / launch chain: one small dependent kernel per tree level (DESIGN.md 5b)"),
-                "compute": compute,
-            },
+            "roofline": roofline,
             "cpu_baseline": cpu,
             "cpu_baseline_all_threads": cpu_mt,
             "host_inclusive": host_inclusive,
@@ -625,8 +887,15 @@ def main():
             "sampler_latency": sampler,
             "draws_100": draws_100,
             "program": info,
+            "nominal_loglik": ll_nominal,
             "kernel_source": kernel_source_hash(),
         }
+        if args.multi_device:
+            rec["config"]["reduction"] = sl.reduction
+        if args.rehearse:
+            rec["rehearsal"] = "every rank on device 0, gloo collectives: a check of the multi-rank path, not a measurement"
+        if synth is not None:
+            rec["synthetic"] = synth
         line = json.dumps(rec)
         print(line, flush=True)
         if args.json_out:
@@ -634,6 +903,9 @@ def main():
                 fp.write(line + "\n")
         if check is not None and not check["ok"]:
             print("bench.py: GPU nominal log-lik disagrees with the CPU port", file=sys.stderr)
+            sys.exit(3)
+        if synth is not None and not synth["nominal_check"]["ok"]:
+            print("bench.py: synthetic rows disagree with the CPU port", file=sys.stderr)
             sys.exit(3)
     if world > 1:
         dist.destroy_process_group()

@@ -7,6 +7,8 @@ point gets an explicit signature, and a missing library is a hard error --
 there is no CPU fallback in the product path.
 """
 import ctypes
+import importlib.abc
+import importlib.util
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
@@ -65,37 +67,50 @@ class PhyloHipError(RuntimeError):
     pass
 
 
-class _TorchAfterEngineGuard:
+_GUARD_MSG = (
+    "phylostan_amd: torch imported after libphylo_hip.so was loaded; torch's bundled HIP runtime cannot "
+    "initialise the GPU after the engine's runtime holds it.  Import torch before phylostan_amd's engine, "
+    "or set PHYLO_WITH_TORCH=1 so that loading the engine imports torch first.")
+
+
+class _GuardLoader(importlib.abc.Loader):
+    def create_module(self, spec):
+        raise ImportError(_GUARD_MSG)
+
+    def exec_module(self, module):  # never reached
+        raise ImportError(_GUARD_MSG)
+
+
+class _TorchAfterEngineGuard(importlib.abc.MetaPathFinder):
     """Import hook installed when the library is loaded in a process that has
     not imported torch.  The PyTorch wheel bundles its own HIP runtime; once
     this library's runtime (ROCm's) holds the GPU, a torch imported later
     fails its GPU initialisation with a misleading "No HIP GPUs are
     available" (INTEGRATION.md, "PyTorch in the same process";
     tools/dbg_torch_after.py).  The guard turns that into a clear error at
-    the ``import torch`` that causes it."""
+    the ``import torch`` that causes it.  It answers ``find_spec`` with a
+    spec whose loader raises, so availability probes
+    (``importlib.util.find_spec("torch")``) still see torch as installed and
+    only an actual import fails."""
 
     def find_spec(self, name, path=None, target=None):
         if name == "torch" and _lib is not None:
-            raise ImportError(
-                "phylostan_amd: torch imported after libphylo_hip.so was loaded; torch's bundled HIP runtime "
-                "cannot initialise the GPU after the engine's runtime holds it.  Import torch before "
-                "phylostan_amd's engine (or set PHYLO_NO_TORCH=1 before loading to disable this guard in a "
-                "process that must not import torch at all).")
+            return importlib.util.spec_from_loader(name, _GuardLoader())
         return None
 
 
 def _order_runtimes():
-    """Make the two HIP runtimes' order correct by construction: import torch
-    (loaded, not initialised: ~1.5 s, no GPU work) before the engine's
-    library when torch is installed; where it is not installed, or
-    PHYLO_NO_TORCH=1 says the process must not import it, install the guard
-    so a later ``import torch`` fails loudly instead of leaving torch without
-    a GPU."""
-    import importlib.util
+    """Keep the two HIP runtimes in a working order.  A process that has
+    already imported torch is fine as it is.  PHYLO_WITH_TORCH=1 imports
+    torch (loaded, not initialised: ~1.5 s, no GPU work) before the library,
+    for a process that will use torch later.  Otherwise nothing is imported
+    -- a CLI or Stan-style consumer pays nothing for torch -- and the guard
+    makes a later ``import torch`` fail loudly instead of leaving torch
+    without a GPU."""
     import sys
     if "torch" in sys.modules:
         return
-    if os.environ.get("PHYLO_NO_TORCH") != "1" and importlib.util.find_spec("torch") is not None:
+    if os.environ.get("PHYLO_WITH_TORCH") == "1":
         import torch  # noqa: F401
         return
     if not any(isinstance(f, _TorchAfterEngineGuard) for f in sys.meta_path):

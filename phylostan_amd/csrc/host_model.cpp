@@ -432,21 +432,29 @@ void phh_strict_post(void* hnd, int n, const double* U, const double* rows, int 
       grate -= 1000.0;
     }
     {  // log-Jacobian of the height transform: sum log(gap) as the log of a
-       // product, renormalised every 8 gaps (no under- or overflow for gaps in
-       // [1e-38, 1e38]); a gap <= 0 gives -inf / NaN as the sum of logs does
+       // product renormalised after every factor (mantissa in [0.5, 1), so no
+       // under- or overflow and no subnormal precision loss for any normal
+       // gap); a gap that is not a positive normal number -- <= 0, NaN,
+       // subnormal -- takes the sum of logs, so -inf / NaN come out exactly
+       // as the reference's sum of logs gives them
       double prod = 1.0;
       int pexp = 0;
+      bool plain = true;
       for (size_t i = 0; i < m.jpar.size(); ++i) {
         const double gap = d.h[m.jpar[i]] - m.jlow[i];
-        prod *= gap;
-        if ((i & 7) == 7) {
-          int ex;
-          prod = std::frexp(prod, &ex);
-          pexp += ex;
-        }
+        plain &= std::isnormal(gap) && gap > 0.0;
+        int ex;
+        prod = std::frexp(prod * gap, &ex);
+        pexp += ex;
         gh[m.jpar[i]] += 1.0 / gap;
       }
-      l += std::log(prod) + pexp * 0.69314718055994530942;
+      if (plain) {
+        l += std::log(prod) + pexp * 0.69314718055994530942;
+      } else {
+        double s = 0.0;
+        for (size_t i = 0; i < m.jpar.size(); ++i) s += std::log(d.h[m.jpar[i]] - m.jlow[i]);
+        l += s;
+      }
     }
     if (m.coal) {  // constant coalescent, theta ~ oneOnX
       for (int i = 0; i < S; ++i) times[i] = m.tip_times[i];

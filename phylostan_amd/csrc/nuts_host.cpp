@@ -15,11 +15,10 @@
 // function Generator.standard_normal calls per element) and uniforms through
 // the bit generator's next_double (Generator.uniform() of [0, 1) is exactly
 // that value), so both implementations draw the same numbers in the same
-// order.  Dot products follow numpy's for short vectors (dot below), so
-// chains of up to 15 dimensions are bitwise equal to nuts.py's; for longer
-// ones energies agree to rounding, and that rounding, amplified by the
-// step-size adaptation, makes long runs drift apart as two runs of the
-// same sampler on different BLAS builds do.
+// order.  Dot products are one sequential sum of rounded products (dot
+// below; nuts.py's _sdot is numpy's strictly sequential cumsum of the same
+// products, and this file is built with -ffp-contract=off), so the chains
+// are bitwise equal to nuts.py's in every dimension, on any CPU and BLAS.
 //
 // Protocol (phn_*): phn_step takes the (lp, grad) of the positions asked
 // for last time and returns the next positions to evaluate, one per chain
@@ -59,13 +58,10 @@ double log_sum_exp(double a, double b) {  // nuts.py:26
   return m + std::log(std::exp(a - m) + std::exp(b - m));
 }
 
-// numpy's 1-D dot (OpenBLAS ddot) accumulates short vectors (n < 16 on the
-// build machine) as one fused multiply-add chain; longer ones use vector
-// accumulators in a CPU-dependent order, where the two implementations agree
-// to rounding only
+// nuts.py _sdot: ((a0 b0 + a1 b1) + a2 b2) + ..., every product rounded
 double dot(const Vec& a, const Vec& b) {
   double s = 0.0;
-  for (size_t i = 0; i < a.size(); ++i) s = std::fma(a[i], b[i], s);
+  for (size_t i = 0; i < a.size(); ++i) s += a[i] * b[i];
   return s;
 }
 
@@ -152,7 +148,7 @@ struct Chain {
   double H(const Point& a) const {  // nuts.py:148
     if (!std::isfinite(a.lp)) return INFINITY;
     double s = 0.0;
-    for (int i = 0; i < dim; ++i) s = std::fma(im[i] * a.p[i], a.p[i], s);
+    for (int i = 0; i < dim; ++i) s += (im[i] * a.p[i]) * a.p[i];
     return -a.lp + 0.5 * s;
   }
 

@@ -3208,8 +3208,9 @@ int phy_create(int S, int P, int C, int rooted, int model, const uint8_t* tipcod
     const size_t pin = (size_t)std::min(max_draws, PIN_DRAWS);
     const size_t outlen_full = (size_t)1 + c->B + 2 * C + 14 + (size_t)16 * C * c->B;
     TRY_C(dalloc(&c->d_in, pin * (c->B + 10 + 2 * C + EIG_LEN)));
-    HIP_C(hipHostMalloc((void**)&c->h_in, sizeof(double) * pin * (c->B + 10 + 2 * C + EIG_LEN), hipHostMallocDefault));
-    HIP_C(hipHostMalloc((void**)&c->h_out, sizeof(double) * pin * outlen_full, hipHostMallocDefault));
+    // portable: a multi-device context's shards all upload from shard 0's staging (multi_enqueue)
+    HIP_C(hipHostMalloc((void**)&c->h_in, sizeof(double) * pin * (c->B + 10 + 2 * C + EIG_LEN), hipHostMallocPortable));
+    HIP_C(hipHostMalloc((void**)&c->h_out, sizeof(double) * pin * outlen_full, hipHostMallocPortable));
     if (env_flag("PHY_DIRECT_OUT", PHY_DIRECT_OUT_DEFAULT)) {
       void* dp = nullptr;
       HIP_C(hipHostGetDevicePointer(&dp, c->h_out, 0));
@@ -3331,6 +3332,18 @@ int phy_create_multi(int S, int P, int C, int rooted, int model, const uint8_t* 
     m->ev.push_back(ev);
   }
   if (!same) {
+    // peer access between shard 0's device and every other: phy_eval_device's input copies
+    // (hipMemcpyPeerAsync) go device to device over xGMI instead of through the host
+    for (int k = 1; k < n_shards; ++k) {
+      int can = 0;
+      if (hipDeviceCanAccessPeer(&can, devices[k], devices[0]) == hipSuccess && can) {
+        (void)hipSetDevice(devices[k]);
+        (void)hipDeviceEnablePeerAccess(devices[0], 0);  // "already enabled" is fine
+        (void)hipSetDevice(devices[0]);
+        (void)hipDeviceEnablePeerAccess(devices[k], 0);
+      }
+    }
+    (void)hipGetLastError();
     int rc = rccl_api(&m->rccl);
     if (rc) return bail(rc);
     m->comm.assign(n_shards, nullptr);

@@ -31,6 +31,16 @@ import time
 import numpy as np
 
 
+def _sdot(a, b):
+    """sum_i a_i b_i as one sequential sum of rounded products: numpy's
+    add.accumulate is a strict left-to-right loop (np.dot's order depends on
+    the BLAS build and the CPU), so csrc/nuts_host.cpp's dot reproduces it
+    bit for bit on any host."""
+    if len(a) == 0:
+        return 0.0
+    return float(np.cumsum(np.multiply(a, b))[-1])
+
+
 def _log_sum_exp(a, b):
     if a == -math.inf:
         return b
@@ -156,7 +166,7 @@ class Chain:
     def _H(self, z):
         if not np.isfinite(z.lp):
             return math.inf
-        return -z.lp + 0.5 * float(np.dot(self.inv_metric * z.p, z.p))
+        return -z.lp + 0.5 * _sdot(self.inv_metric * z.p, z.p)
 
     def _evolve(self, z, eps):
         """expl_leapfrog: one step in place; yields the new q for (lp, grad)."""
@@ -199,7 +209,7 @@ class Chain:
 
     @staticmethod
     def _criterion(ps_minus, ps_plus, rho):
-        return ps_plus.dot(rho) > 0 and ps_minus.dot(rho) > 0
+        return _sdot(ps_plus, rho) > 0 and _sdot(ps_minus, rho) > 0
 
     def _build_tree(self, depth, z, H0, sign, st):
         """Returns (valid, z_propose, p_sharp_beg, p_sharp_end, rho, p_beg,

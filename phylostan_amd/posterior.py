@@ -521,7 +521,8 @@ class Posterior:
             cnt, bl, mv, sel = self._fast.pre(U)
             tok = {"fast": True, "U": U, "sel": sel, "propto": propto, "need_grad": need_grad}
             if cnt:
-                if hasattr(self.lik, "submit_rows") and cnt <= 64:
+                if hasattr(self.lik, "submit_rows") and cnt <= min(getattr(self.lik, "max_draws", 64),
+                                                                   getattr(self.lik, "_STAGE_DRAWS", 64)):
                     self.lik.submit_rows(bl, mv)
                     tok["async"] = True
                 else:

@@ -194,3 +194,47 @@ def random_case(seed, S=12, P=100, C=3, model="GTR", rooted=True, caterpillar=Fa
         rates = np.ones(6)
     rs, ps = models.weibull_site_rates(rng.uniform(0.3, 2.0), C)
     return Case("rand%d" % seed, codes, w, peel, rooted, model, C, blens, freqs, rates, rs, ps)
+
+
+def load_zero_rate_points():
+    """Site-rate variants with a zero-rate or free-weight category (+I with
+    Weibull, +I with one category, discrete heterogeneity) evaluated by the
+    reference's scripts/phylo.py (tests/golden/make_golden.py
+    ``zero_rate_fixture``)."""
+    with open(os.path.join(GOLDEN, "phylo_zero_rate.json")) as fp:
+        return json.load(fp)["points"]
+
+
+def zero_rate_case(point):
+    d = load_layout(point["dataset"])
+    return Case("zr_%s_%s_%s" % (point["dataset"], point["model"], point["kind"]), d["tipbits"], d["weights"],
+                d["peel"] - 1, True, point["model"], point["C"], point["blens"], point["freqs"], point["rates"],
+                point["rs"], point["ps"])
+
+
+def zero_rate_dpinv(point):
+    """(drs/dpinv, dps/dpinv) of the point's +I site rates
+    (generate_script.py:250-266, :1231-1240) by central differences of the
+    host restatement (exact to ~1e-10 relative)."""
+    from tests.golden.make_golden import _zero_rate_rates
+    h = 1e-6
+    a = _zero_rate_rates(point["kind"], point["pinv"] + h, point.get("wshape"))
+    b = _zero_rate_rates(point["kind"], point["pinv"] - h, point.get("wshape"))
+    return (np.asarray(a[0]) - np.asarray(b[0])) / (2 * h), (np.asarray(a[1]) - np.asarray(b[1])) / (2 * h)
+
+
+def zero_rate_errors(res_like, pt):
+    """Max relative errors of an evaluation's site-rate and branch gradients
+    against the point's reference finite differences."""
+    errs = {}
+    for key in ("grad_rs", "grad_ps"):
+        ref = np.asarray(pt[key])
+        errs[key[5:]] = float(np.max(np.abs(np.asarray(res_like[key]) - ref)) / np.max(np.abs(ref)))
+    gb = np.asarray(res_like["grad_blens"])[pt["branches"]]
+    ref = np.asarray(pt["grad_blens"])
+    errs["blens"] = float(np.max(np.abs(gb - ref)) / np.max(np.abs(ref)))
+    if "grad_pinv" in pt:
+        drs, dps = zero_rate_dpinv(pt)
+        g = float(np.dot(res_like["grad_rs"], drs) + np.dot(res_like["grad_ps"], dps))
+        errs["pinv"] = abs(g - pt["grad_pinv"]) / abs(pt["grad_pinv"])
+    return errs

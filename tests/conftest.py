@@ -9,6 +9,11 @@ if ROOT not in sys.path:
 
 from tests import report  # noqa: E402
 
+try:  # torch's bundled HIP runtime must load before the engine's: the GPU tests
+    import torch  # noqa: F401,E402  use torch tensors after engine contexts exist
+except ImportError:
+    pass
+
 
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (run on the GPU box via gpurun)")

@@ -443,7 +443,131 @@ def grad_fixture(phylo, specs):
     return out
 
 
+# Zero-rate and free-weight categories (site-rate variants other than the
+# configs' plain Weibull): -I with Weibull (generate_script.py:250-266: rs[1] = 0,
+# ps[1] = pinv), -I with one category (:1231-1240: C = 2, rs = (0, 1/(1-pinv))),
+# and --heterogeneity discrete (:1221-1230: ps a simplex, rs = x / sum(ps .* x)).
+ZERO_RATE_POINTS = [
+    # dataset, model, kind, pinv / (ps, rate_unscaled), shape
+    ("fluA", "HKY", "pinv_weibull", 0.2, 0.488),
+    ("HCV", "GTR", "pinv_weibull", 0.3, 0.5),
+    ("HCV", "GTR", "pinv_single", 0.25, None),
+    ("fluA", "HKY", "discrete", ([0.1, 0.2, 0.3, 0.4], [0.05, 0.15, 0.3, 0.5]), None),
+]
+
+
+def _zero_rate_rates(kind, arg, shape):
+    from phylostan_amd import models
+    if kind == "pinv_weibull":
+        return models.weibull_pinv_site_rates(shape, arg, 4)
+    if kind == "pinv_single":
+        return np.array([0.0, 1.0 / (1.0 - arg)]), np.array([arg, 1.0 - arg])
+    ps, x = np.array(arg[0]), np.array(arg[1])
+    return x / np.sum(ps * x), ps
+
+
+def zero_rate_fixture(phylo, specs):
+    """Log-likelihoods (total and per pattern) and central differences of the
+    reference's scripts/phylo.py pruner (per category, edges b r_c -- a zero
+    rate gives zero-length edges, P = I) combined as the mixture line
+    generate_script.py:1006-1010, for the site-rate variants above: d/dpinv
+    through rs and ps (the +I forms), d/drs_c and d/dps_c as free variables
+    (every variant; at r_0 = 0 the central difference straddles zero), and
+    four branch lengths.  Same points' data as the mixture fixture (fluA at
+    the README point, HCV at SConstruct:218's)."""
+    from phylostan_amd import models
+    out = {"source": "scripts/phylo.py:240-296 per category, mixture generate_script.py:1006-1010; site rates "
+                     "generate_script.py:250-266 (+I Weibull), :1231-1240 (+I, C = 1), :1221-1230 (discrete)",
+           "points": []}
+
+    def deriv(f, x0, h):
+        d1 = (f(x0 + h) - f(x0 - h)) / (2 * h)
+        d2 = (f(x0 + h / 2) - f(x0 - h / 2)) / h
+        return (4.0 * d2 - d1) / 3.0
+
+    with open(os.path.join(HERE, "phylo_mixture.json")) as fp:
+        mix = {p["dataset"]: p for p in json.load(fp)["points"]}
+    for name, model, kind, arg, shape in ZERO_RATE_POINTS:
+        pt = mix[name]
+        tpath, apath = specs[name][:2]
+        layout = np.load(os.path.join(HERE, "%s_layout.npz" % name), allow_pickle=False)
+        tree = treeio.read_tree(tpath)
+        tree.resolve_polytomies(update_bipartitions=True)
+        aln = treeio.read_alignment(apath)
+        phylo.setup_indexes(tree, _Alignment({t.label: _Seq(aln[t.label]) for t in tree.taxon_namespace}))
+        taxa = [t.label for t in tree.taxon_namespace]
+        alignment, w = _pattern_alignment(layout, taxa)
+        blens = np.array(pt["blens"], dtype=np.float64)
+        rates, freqs = list(pt["rates"]), list(pt["freqs"])
+        rs, ps = _zero_rate_rates(kind, arg, shape)
+
+        def site(bl, rsv, psv):
+            lik = 0.0
+            for c in range(len(rsv)):
+                for nd in tree.postorder_node_iter():
+                    if nd.parent_node is not None:
+                        nd.edge_length = float(bl[nd.index]) * float(rsv[c])
+                lik = lik + float(psv[c]) * _phylo_root_site_lik(phylo, tree, alignment,
+                                                                 phylo.GTR(list(rates), list(freqs)))
+            return np.log(lik)
+
+        def F(bl=blens, rsv=rs, psv=ps):
+            return float(np.dot(w, site(bl, rsv, psv)))
+
+        sl = site(blens, rs, ps)
+        rec = {"dataset": name, "model": model, "kind": kind, "rooted": True, "C": len(rs), "rates": rates,
+               "freqs": freqs, "rs": list(rs), "ps": list(ps), "blens": blens.tolist(),
+               "loglik": float(np.dot(w, sl)), "site_ll": sl.tolist()}
+        if kind != "discrete":
+            rec["pinv"] = arg
+            rec["grad_pinv"] = deriv(lambda x: F(rsv=_zero_rate_rates(kind, x, shape)[0],
+                                                 psv=_zero_rate_rates(kind, x, shape)[1]), arg, 1e-4)
+        if shape is not None:
+            rec["wshape"] = shape
+        grs, gps = [], []
+        for c in range(len(rs)):
+            def fr(x, c=c):
+                r = np.array(rs, dtype=np.float64)
+                r[c] = x
+                return F(rsv=r)
+
+            def fp_(x, c=c):
+                q = np.array(ps, dtype=np.float64)
+                q[c] = x
+                return F(psv=q)
+            if rs[c] == 0.0:  # phylo.GTR.p_t takes |P| (scripts/phylo.py:22): the reference has a kink
+                # at t = 0, so the zero rate's derivative is one-sided (rates >= 0), forward Richardson
+                h = 1e-6
+                d1 = (fr(h) - fr(0.0)) / h
+                d2 = (fr(h / 2) - fr(0.0)) / (h / 2)
+                grs.append(2.0 * d2 - d1)
+            else:
+                grs.append(deriv(fr, rs[c], 1e-4 * rs[c]))
+            gps.append(deriv(fp_, ps[c], 1e-4 * ps[c]))
+        rec["grad_rs"], rec["grad_ps"] = grs, gps
+        br = np.unique(np.linspace(0, blens.size - 1, 4).round().astype(int)).tolist()
+        gb = []
+        for b in br:
+            def fb(x, b=b):
+                bl = blens.copy()
+                bl[b] = x
+                return F(bl=bl)
+            gb.append(deriv(fb, blens[b], 1e-3 * max(blens[b], 1e-4)))
+        rec["branches"], rec["grad_blens"] = br, gb
+        out["points"].append(rec)
+        print(name, model, kind, "loglik %.10f" % rec["loglik"], {k: v for k, v in rec.items()
+                                                                  if k.startswith("grad")})
+    return out
+
+
 def main():
+    if len(sys.argv) > 1 and sys.argv[1] == "zero_rate":  # only the site-rate variants' fixture
+        ex = os.path.join(REF, "examples")
+        specs = {"fluA": (os.path.join(ex, "fluA", "fluA.tree"), os.path.join(ex, "fluA", "fluA.fa")),
+                 "HCV": (os.path.join(ex, "HCV", "HCV.tree"), os.path.join(ex, "HCV", "HCV.nexus"))}
+        with open(os.path.join(HERE, "phylo_zero_rate.json"), "w") as fp:
+            json.dump(zero_rate_fixture(_import_reference_phylo(), specs), fp)
+        return
     if len(sys.argv) > 1 and sys.argv[1] == "grad":  # only the reference FD gradients
         ex = os.path.join(REF, "examples")
         specs = {"fluA": (os.path.join(ex, "fluA", "fluA.tree"), os.path.join(ex, "fluA", "fluA.fa")),

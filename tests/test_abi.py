@@ -73,29 +73,32 @@ def test_stale_build_is_refused(tmp_path, monkeypatch):
 
 
 def test_torch_after_engine_is_a_clear_error():
-    """Run in a fresh interpreter: with PHYLO_NO_TORCH=1 the engine loads
-    without torch, and a later `import torch` raises the guard's ImportError
-    instead of leaving torch without a GPU; by default load() imports torch
-    first, so the order is right by construction."""
+    """Run in a fresh interpreter: by default the engine loads without torch
+    (a non-torch consumer pays nothing), a probe still finds torch, and a
+    later `import torch` raises the guard's ImportError instead of leaving
+    torch without a GPU; with PHYLO_WITH_TORCH=1 load() imports torch first,
+    so the order is right by construction."""
     import subprocess
     import sys
     from phylostan_amd import _lib
     if not os.path.exists(_lib.LIB_PATH):
         pytest.skip("HIP library not built")
-    code = ("import sys; sys.path.insert(0, %r)\n"
+    code = ("import sys, importlib.util; sys.path.insert(0, %r)\n"
             "from phylostan_amd import _lib\n"
             "_lib.load()\n"
             "print('torch loaded before engine:', 'torch' in sys.modules)\n"
+            "print('probe finds torch:', importlib.util.find_spec('torch') is not None)\n"
             "try:\n"
             "    import torch\n"
             "    print('import ok')\n"
             "except ImportError as e:\n"
             "    print('guard:', 'imported after' in str(e))\n") % ROOT
-    env = dict(os.environ, PHYLO_NO_TORCH="1")
+    env = {k: v for k, v in os.environ.items() if k not in ("PHYLO_WITH_TORCH", "PHYLO_NO_TORCH")}
     out = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=300)
     assert "torch loaded before engine: False" in out.stdout, out.stdout + out.stderr
+    assert "probe finds torch: True" in out.stdout, out.stdout + out.stderr
     assert "guard: True" in out.stdout, out.stdout + out.stderr
-    env.pop("PHYLO_NO_TORCH")
+    env["PHYLO_WITH_TORCH"] = "1"
     out = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=300)
     assert "torch loaded before engine: True" in out.stdout, out.stdout + out.stderr
     assert "import ok" in out.stdout, out.stdout + out.stderr

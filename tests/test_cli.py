@@ -283,3 +283,19 @@ def test_ds1_reference_form_tree_round_trips(tmp_path):
     np.testing.assert_array_equal(d.peel0, lay["peel"] - 1)
     np.testing.assert_array_equal(d.tipcodes, lay["tipbits"])
     np.testing.assert_array_equal(d.weights, lay["weights"])
+
+
+def test_config3_hcv_skyride_columns_cpu(tmp_path):
+    """Config 3's run shape (SConstruct:215-218: GTR+W4, strict clock at a
+    fixed --rate, skyride) on the CPU stand-in, 150 iterations: the skyride's
+    thetas.k (S-1 of them) and tau columns are written (the GPU test runs it
+    to convergence)."""
+    t, a = fixture_files.write_dataset("HCV", str(tmp_path))
+    out = str(tmp_path / "hcv")
+    post, lines = _run(["-s", str(tmp_path / "x.stan"), "-m", "GTR", "-C", "4", "--clock", "strict",
+                        "--rate", "7.9e-4", "--coalescent", "skyride", "-t", t, "-i", a, "-o", out, "-S", "3",
+                        "--iter", "150", "--elbo_samples", "10", "--samples", "20", "--eta", "0.1"])
+    header, data = stan_io.read_samples(out)
+    assert "thetas.62" in header and "thetas.63" not in header and "tau" in header
+    assert "rate" not in header and "heights.62" in header and "rates.6" in header
+    assert data.shape == (21, len(header)) and np.isfinite(data).all()

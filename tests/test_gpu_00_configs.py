@@ -300,3 +300,56 @@ def test_fluA_nuts_config5_full():
         assert lo <= m <= hi, "%s posterior mean %g outside the reference's 95%% CI (%g, %g)" % (key, m, lo, hi)
     report.record("config 5 fluA NUTS 4x(1000+1000) in %.1f s: posterior means inside README CIs: %s"
                   % (wall, ", ".join("%s %.4g" % kv for kv in means.items())))
+
+
+ZERO_RATE_IDS = ["fluA_HKY_I_W4", "HCV_GTR_I_W4", "HCV_GTR_I", "fluA_HKY_discrete"]
+
+
+@pytest.mark.parametrize("k", range(4), ids=ZERO_RATE_IDS)
+def test_zero_rate_categories_vs_reference(k):
+    """A zero-rate category on the device: -I with Weibull
+    (generate_script.py:250-266: rs[0] = 0, ps[0] = pinv; t = 0, so P = I and
+    the Q-parameter chain rule's Phi takes its tie branch t e^{lambda t} = 0),
+    -I with one category (:1231-1240, C = 2) and discrete heterogeneity
+    (:1221-1230, free ps).  Every engine -- the quad sweep (a sampler's call),
+    the column sweep at one and two columns per lane, the class sweep, and a
+    32-draw device-path batch -- against the reference's scripts/phylo.py
+    (per-pattern and total log L, rel 1e-10), the oracle (every gradient, rel
+    1e-9; the exchangeability / frequency gradients 1e-8) and the reference's
+    finite differences of d/drs, d/dps, d/dblens and d/dpinv (rel 1e-6,
+    tests/golden/phylo_zero_rate.json)."""
+    pt = cases.load_zero_rate_points()[k]
+    case = cases.zero_rate_case(pt)
+    ref = case.oracle()
+    worst = {}
+    for engine, cols in (("quad", 0), ("pattern", 1), ("pattern", 2), ("class", 0)):
+        eng = _engine(case)
+        eng.set_engine("class" if engine == "class" else "pattern")
+        if cols:
+            eng.set_tuning(cols=cols)
+        res = eng.evaluate(case.blens, case.model_vec(), site_ll=True)
+        e = errors(res, ref, case.model)
+        eq = q_param_error(case, res, ref)
+        check(e, eq)
+        e_site = _site_rel(res.site_ll, pt["site_ll"])
+        e_ll = abs(res.loglik - pt["loglik"]) / abs(pt["loglik"])
+        assert e_site <= RTOL_LL and e_ll <= RTOL_LL, (engine, e_site, e_ll)
+        fd = cases.zero_rate_errors({"grad_rs": res.grad_rs, "grad_ps": res.grad_ps,
+                                     "grad_blens": res.grad_blens}, pt)
+        assert all(v <= 1e-6 for v in fd.values()), (engine, fd)
+        for key, v in list(fd.items()) + [("loglik", e_ll), ("site_ll", e_site), ("dLdP", e["dLdP"]), ("Q", eq)]:
+            worst[key] = max(worst.get(key, 0.0), v)
+    # the batched device path (column sweep, one workgroup per draw): 32 draws, the point in every row
+    n = 32
+    eng = _engine(case, max_draws=n)
+    rows = eng.evaluate_rows(np.repeat(case.blens[None], n, 0), np.repeat(case.model_vec()[None], n, 0))
+    single = _engine(case)
+    single.set_tuning(cols=1)
+    r1 = single.evaluate_rows(case.blens[None], case.model_vec()[None])[0]
+    assert np.all(rows == rows[0])
+    assert _rel(rows[0], r1) <= 1e-12
+    report.record("site-rate variant %s: vs scripts/phylo.py loglik %.1e site_ll %.1e | vs reference FD %s | "
+                  "dLdP vs oracle %.1e Q-params %.1e (quad, K=1, K=2, class, 32-draw batch)"
+                  % (ZERO_RATE_IDS[k], worst["loglik"], worst["site_ll"],
+                     " ".join("%s %.1e" % (kk, worst[kk]) for kk in ("rs", "ps", "blens", "pinv") if kk in worst),
+                     worst["dLdP"], worst["Q"]))

@@ -199,3 +199,46 @@ def test_config1_ds1_jc69_unrooted_meanfield(tmp_path, capsys):
     ran = open(out + ".trees").read()
     parsed = open(str(tmp_path / "parsed.trees")).read()
     assert ran.count("tree ") == 1001 and ran == parsed
+
+
+def test_config3_hcv_gtr_skyride_as_the_reference_runs_it(tmp_path, capsys):
+    """BASELINE config 3 as the reference runs it (examples/SConstruct:215-218):
+    `phylostan build -m GTR -C 4 --clock strict --coalescent skyride`, then
+    `phylostan run -m GTR -C 4 --clock strict --rate 7.9e-4 --coalescent
+    skyride` on HCV (contemporaneous tips, the clock rate fixed), every
+    gradient from the GPU engine, meanfield ADVI at eta 0.1 (no adaptation:
+    the run is a function of the seed).  The posterior is parity-unpinned (the
+    reference publishes no HCV numbers); this checks the run's contract:
+    Stan's progress lines, an ELBO that rises and stops by tol_rel_obj, the
+    skyride's `thetas.k` / `tau` columns beside `heights.k`, `rates.k`,
+    `freqs.k`, and `parse` giving the .trees file `run` wrote."""
+    import re
+    from phylostan_amd import cli, stan_io
+    t, a = fixture_files.write_dataset("HCV", str(tmp_path))
+    script = str(tmp_path / "hcv.stan")
+    assert cli.main(["build", "-m", "GTR", "-C", "4", "--clock", "strict", "--coalescent", "skyride",
+                     "-s", script]) == 0
+    out = str(tmp_path / "hcv")
+    capsys.readouterr()
+    cli.main(["run", "-i", a, "-t", t, "-s", script, "-o", out, "-m", "GTR", "-C", "4", "--clock", "strict",
+              "--rate", "7.9e-4", "--coalescent", "skyride", "--eta", "0.1", "--seed", "1"])
+    printed = capsys.readouterr().out
+    prog = [(int(m.group(1)), float(m.group(2))) for m in re.finditer(r"\s+(\d+)\s+(-\d+\.\d+)", printed)]
+    assert len(prog) >= 5, printed[:2000]
+    elbo = np.array([e for _, e in prog])
+    assert np.isfinite(elbo).all() and elbo[-1] > elbo[0]
+    assert "ELBO CONVERGED" in printed and prog[-1][0] < 100000
+    header, data = stan_io.read_samples(out)
+    S = 63
+    for k in (1, S - 1):
+        assert "thetas.%d" % k in header
+    assert "thetas.%d" % S not in header and "tau" in header
+    assert "heights.%d" % (S - 1) in header and "rates.6" in header and "freqs.4" in header
+    assert "rate" not in header  # --rate fixes the clock rate: no rate parameter
+    assert data.shape == (1001, len(header)) and np.isfinite(data).all()
+    tau = data[:, header.index("tau")]
+    assert np.all(tau > 0)
+    cli.main(["parse", "--samples", out, "-t", t, "-o", str(tmp_path / "parsed.trees")])
+    ran = open(out + ".trees").read()
+    parsed = open(str(tmp_path / "parsed.trees")).read()
+    assert ran.count("tree ") == 1001 and ran == parsed

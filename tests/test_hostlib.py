@@ -159,3 +159,30 @@ def test_native_strict_posterior_not_used_outside_its_family():
                dict(model="HKY", categories=4)):
         spec = ModelSpec(**kw)
         assert Posterior(spec, tree, RowsLik(2 * S - 2, spec.C))._fast is None
+
+
+def test_native_height_jacobian_tiny_gaps():
+    """Nested tiny proportions (early-warmup shapes) on a tree of
+    contemporaneous tips: the gaps shrink geometrically down the tree but stay
+    positive normal numbers, so the log-Jacobian of the height transform is
+    finite; the native product must not underflow where the numpy sum of logs
+    does not (host_model.cpp)."""
+    kw = dict(model="GTR", categories=4, clock="strict", estimate_rate=False, coalescent="constant",
+              heterochronous=False)
+    post = _posterior("HCV", **kw)
+    assert post._nat is not None
+    ref = _posterior("HCV", **kw)
+    ref._nat = None
+    ref._fast = None
+    rng = np.random.default_rng(5)
+    us = [-46.0, -20.0, -6.9, -3.0]
+    U = np.stack([post.initial_point(rng) for _ in us])
+    sl = next(p.sl for p in post.params if p.name == "props")
+    for i, u in enumerate(us):
+        U[i, sl] = u  # every proportion ~ e^u
+    with np.errstate(all="ignore"):
+        lp_n, g_n = post.log_prob_grad(U)
+        lp_r, g_r = ref.log_prob_grad(U)
+    assert np.all(np.isfinite(lp_r))
+    np.testing.assert_allclose(lp_n, lp_r, rtol=1e-11)
+    np.testing.assert_allclose(g_n, g_r, rtol=1e-9, atol=1e-9 * np.abs(g_r).max())

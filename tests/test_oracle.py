@@ -282,3 +282,24 @@ def test_oracle_gradients_vs_reference_fd(k):
     errs = reference_grad_errors({"grad_blens": ref["grad_blens"], "grad_rs": ref["grad_rs"], "grad_rates": gr,
                                   "grad_freqs": gf}, pt, case)
     assert all(v <= REF_GRAD_RTOL for v in errs.values()), errs
+
+
+@pytest.mark.parametrize("k", range(4), ids=["fluA_HKY_I_W4", "HCV_GTR_I_W4", "HCV_GTR_I", "fluA_HKY_discrete"])
+def test_oracle_zero_rate_categories_vs_reference(k):
+    """Zero-rate (+I) and free-weight (discrete) categories: the oracle's
+    per-pattern / total log L against the reference's scripts/phylo.py at rel
+    1e-10, and its d/drs, d/dps, d/dblens and d/dpinv (through rs and ps)
+    against the reference's central differences at 1e-6
+    (tests/golden/phylo_zero_rate.json); the C port agrees with the oracle."""
+    from oracle import cpu
+    from phylostan_amd import models
+    pt = cases.load_zero_rate_points()[k]
+    case = cases.zero_rate_case(pt)
+    ref = case.oracle()
+    assert abs(ref["loglik"] - pt["loglik"]) <= 1e-10 * abs(pt["loglik"])
+    np.testing.assert_allclose(ref["site_ll"], pt["site_ll"], rtol=1e-10)
+    errs = cases.zero_rate_errors(ref, pt)
+    assert all(v <= REF_GRAD_RTOL for v in errs.values()), errs
+    out, _ = cpu.evaluate(case.tipcodes, case.weights, case.peel0, True, models.MODEL_IDS[case.model],
+                          case.model_vec(), case.blens, case.C)
+    assert abs(out[0] - ref["loglik"]) <= 1e-12 * abs(ref["loglik"])
