@@ -534,6 +534,9 @@ def main():
     cpu_group = None
     if args.rehearse:
         local = 0
+        # the ranks share one GPU: the class sweep's dataflow launch wants its grid resident, so the
+        # rehearsal takes the level launches (phy_set_flow); the multidev child inherits this
+        os.environ["PHY_FLOW"] = "0"
     if world > 1:
         torch.cuda.set_device(local)
         if args.rehearse:

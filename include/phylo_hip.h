@@ -238,6 +238,18 @@ int phy_set_output(phy_ctx* ctx, int compact);
 int phy_set_engine(phy_ctx* ctx, int mode);
 int phy_engine(const phy_ctx* ctx);
 
+/* The class sweep's launch form: 1 (default; PHY_FLOW=0 at phy_create sets
+ * 0) = ONE dataflow launch for the whole sweep -- forward chunks, root, the
+ * reverse's tile reductions, span fix-ups and chunks as work items that wait
+ * only for the items they read (per-node completion counters, no grid-wide
+ * barrier); 0 = one launch per tree level and phase.  Results are bitwise the
+ * same.  Shards of a same-device phy_create_multi context always use the
+ * level launches (their launches run concurrently).  phy_flow returns 1 when
+ * the next class-sweep launch is the dataflow one.  No reference counterpart
+ * (a launch mechanism for the column-reuse idea of pruner/tree.cpp:140-174). */
+int phy_set_flow(phy_ctx* ctx, int on);
+int phy_flow(const phy_ctx* ctx);
+
 /* Class-plan facts (zeros when no plan is built): non-root subtree classes
  * (the class sweep's forward work per category), levels (the root's level),
  * root classes (distinct site patterns by tip state), contributions (sum over

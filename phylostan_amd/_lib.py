@@ -56,6 +56,8 @@ SIGNATURES = {
     "phy_set_engine": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
     "phy_set_output": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
     "phy_engine": (ctypes.c_int, [ctypes.c_void_p]),
+    "phy_set_flow": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
+    "phy_flow": (ctypes.c_int, [ctypes.c_void_p]),
     "phy_class_info": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_longlong), _c_int_p, _c_int_p,
                                       ctypes.POINTER(ctypes.c_longlong), ctypes.POINTER(ctypes.c_longlong),
                                       _c_int_p, _c_int_p]),

@@ -1892,6 +1892,33 @@ __global__ void __launch_bounds__(QG_THREADS) qgrad_kernel(FinArgs a) {
 constexpr int QFIN_THREADS = 256;
 constexpr int QFIN_ITEMS = QFIN_THREADS / 4;  // (c, b) items per workgroup
 constexpr int QFIN_SLOTS = 16;                // workgroup slots per draw it takes
+// HANDOFF.  The split epilogues (qfin_kernel, cls_epi_kernel) hand per-
+// workgroup partials to the draw's last-arriving workgroup inside one launch:
+// every hand-off byte is stored write-through (sc1: __hip_atomic_store
+// relaxed/agent), every storing wave drains vmcnt, a workgroup barrier, then
+// ONE lane's relaxed agent-scope ticket add; the workgroup whose add returns
+// the last ticket reads the hand-offs with sc1 loads only (relaxed agent-scope
+// atomic loads).  On gfx950 that is the sc1 form of cdna_hip_programming.md
+// Guideline 16 / MI355X_MICROARCH.md "Valid forms" row 1: sc1 stores leave
+// the producer's L2 at once, sc1 loads bypass the reader's L1, and the add is
+// issued after the drain -- the reader cannot see a stale copy.  It is
+// ISA-level, not a C++-model, guarantee (relaxed atomics on both sides).  The
+// model-level form adds ONE agent-scope acquire in the last workgroup after
+// its ticket (the guide's R1 consume recipe; the producers' sc1 payload needs
+// no release fence): PHY_HANDOFF_ACQUIRE=1 at build time selects it, measured
+// in DESIGN.md (it sits on the call's critical path); the default keeps the
+// sc1 form, guarded by tests/test_gpu_quad.py / test_gpu_class.py stress tests
+// (10^4 calls, rows compared bitwise, one process).
+#ifndef PHY_HANDOFF_ACQUIRE
+#define PHY_HANDOFF_ACQUIRE 0
+#endif
+__device__ __forceinline__ void handoff_acquire(bool last) {
+  if (PHY_HANDOFF_ACQUIRE && last) {
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the invalidate done before the barrier releases the others
+  }
+}
+
 struct QfinArgs {
   FinArgs f;
   double* part;              // [draw][nspl][16 + C] hand-offs: M partial, sum_b b <G, QP> per category
@@ -2051,14 +2078,15 @@ __global__ void __launch_bounds__(QFIN_THREADS) qfin_kernel(QfinArgs qa) {
   if (tid == 0) {
     const unsigned long long old = __hip_atomic_fetch_add(qa.cnt + draw, 1ull, __ATOMIC_RELAXED,
                                                           __HIP_MEMORY_SCOPE_AGENT);
-    s_last = ((old + 1) % (unsigned long long)nspl) == 0;
+    const bool last = ((old + 1) % (unsigned long long)nspl) == 0;
+    handoff_acquire(last);
+    s_last = last;
   }
   __syncthreads();
   if (!s_last) return;
   // the draw's last workgroup: every hand-off was stored sc1 and drained
-  // before its ticket, and EVERY load of one here is an sc1 load
-  // (agent-scope atomic), so no acquire fence (cdna_hip_programming.md
-  // Guideline 16, the sc1-load form); the other loads read launch inputs
+  // before its ticket, and EVERY load of one here is an sc1 load (HANDOFF
+  // note above handoff_acquire); the other loads read launch inputs
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
   const double* pp = qa.part + (size_t)draw * nspl * (16 + C);
   auto ld1 = [](const double* q) { return __hip_atomic_load(q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); };
@@ -2147,6 +2175,12 @@ struct phy_ctx {
   // engine_pref 0 = automatic, 1 = pattern, 2 = class
   int engine = 0, engine_pref = 0;
   ClassEngine* ce = nullptr;
+  // the class sweep as one dataflow launch (cls_flow_kernel) instead of level
+  // launches: PHY_FLOW=0 / phy_set_flow(ctx, 0) turn it off; off for the
+  // shards of a same-device multi context (their launches run concurrently,
+  // and the flow grid must be resident); flow_wgs = its resident grid
+  bool flow_pref = true, flow_ok = true;
+  int flow_wgs[2] = {0, 0};  // [root has a tip child]: that variant's resident grid
   MultiState* ms = nullptr;  // a multi-device context (phy_create_multi): its shards do the work
   int compact = 0;             // output rows without the dL/dP block (phy_set_output)
   double* d_grows = nullptr;   // dL/dP rows when compact: [max_draws][16 C B]
@@ -2625,6 +2659,12 @@ int select_engine(phy_ctx* c) {
   return PHY_OK;
 }
 
+// The class sweep runs as the dataflow launch (cls_flow_kernel) when it is
+// preferred and allowed and the categories fit its workgroup (C waves <= 16).
+bool flow_applies(const phy_ctx* ctx) {
+  return ctx->flow_pref && ctx->flow_ok && ctx->C <= 16 && ctx->flow_wgs[0] > 0 && ctx->flow_wgs[1] > 0;
+}
+
 // HIP events around the timed part of one launch (phy_timing_start)
 int timing_begin(phy_ctx* ctx, hipStream_t st, hipEvent_t* e0, hipEvent_t* e1) {
   if (ctx->ev_used + 2 > (int)ctx->ev.size()) {
@@ -2660,23 +2700,35 @@ int launch_class(phy_ctx* ctx, int n, const double* d_blens, const double* d_mod
   ClassArgs a = class_args(e, ctx->d_pmat, d_model, ctx->extra);
   const int dcn = n * C;
   hipEvent_t e0 = nullptr, e1 = nullptr;
+  const bool flow = flow_applies(ctx);
+  if (flow) {  // counters zeroed on this stream, then the whole sweep as one dataflow launch
+    HIP_TRY(hipMemsetAsync(e->d_fcnt, 0, (4 + (size_t)n * e->ncnt) * sizeof(unsigned), st));
+  }
   if (ctx->timing && (rc = timing_begin(ctx, st, &e0, &e1))) return rc;
-  if (e->Lc > 0)  // levels 1..Lc: one workgroup per (bottom clade, dc)
+  if (flow) {
+    const FlowArgs fa{e->d_items, e->nitems, n, e->d_fcnt + 4, e->ncnt, e->d_fcnt};
+    const long long total = (long long)e->nitems * n;
+    const int grid = (int)std::min<long long>(total, (long long)ctx->flow_wgs[e->root_tips ? 1 : 0]);
+    auto fk = C <= 4 ? (e->root_tips ? cls_flow_kernel<256, true> : cls_flow_kernel<256, false>)
+                     : (e->root_tips ? cls_flow_kernel<1024, true> : cls_flow_kernel<1024, false>);
+    hipLaunchKernelGGL(fk, dim3(std::max(grid, 1)), dim3(C * WAVE), 0, st, a, fa);
+  }
+  if (!flow && e->Lc > 0)  // levels 1..Lc: one workgroup per (bottom clade, dc)
     hipLaunchKernelGGL(cls_clade_fwd_kernel, dim3(e->nclade, dcn), dim3(CLADE_THREADS), 0, st, a,
                        (const CladeLevel*)e->d_clade, e->Lc);
-  for (int l = e->Lc + 1; l < e->levels; ++l) {
+  for (int l = e->Lc + 1; l < e->levels && !flow; ++l) {
     const ClassLevel& L = e->lv[l];
     if (!L.nchunk) continue;
     a.first = L.chunk0;
     a.count = L.nchunk;
     hipLaunchKernelGGL(cls_fwd_kernel, dim3((L.nchunk + CLS_WPG - 1) / CLS_WPG, dcn), dim3(CLS_THREADS), 0, st, a);
   }
-  {
+  if (!flow) {
     auto rk = C <= 4 ? (e->root_tips ? cls_root_kernel<256, true> : cls_root_kernel<256, false>)
                      : (e->root_tips ? cls_root_kernel<1024, true> : cls_root_kernel<1024, false>);
     hipLaunchKernelGGL(rk, dim3(e->nrootch, n), dim3(C * WAVE), 0, st, a);
   }
-  for (int l = e->levels - 1; l > e->Lc; --l) {
+  for (int l = e->levels - 1; l > e->Lc && !flow; --l) {
     const ClassLevel& L = e->lv[l];
     if (L.ntile) {
       a.first = L.tile0;
@@ -2692,7 +2744,7 @@ int launch_class(phy_ctx* ctx, int n, const double* d_blens, const double* d_mod
       hipLaunchKernelGGL(cls_rev_kernel, dim3((L.nchunk + CLS_WPG - 1) / CLS_WPG, dcn), dim3(CLS_THREADS), 0, st, a);
     }
   }
-  if (e->Lc > 0) {
+  if (!flow && e->Lc > 0) {
     if (e->nrtile)
       hipLaunchKernelGGL(cls_red_list_kernel, dim3((e->nrtile + CLS_WPG - 1) / CLS_WPG, dcn), dim3(CLS_THREADS), 0, st, a,
                          (const int*)e->d_rtile, e->nrtile);
@@ -2711,7 +2763,8 @@ int launch_class(phy_ctx* ctx, int n, const double* d_blens, const double* d_mod
   const size_t ncb = (size_t)n * C * B;
   EpiArgs ea{e->d_gpart, e->d_gbase, e->d_gcount, e->d_sslot, ctx->d_pmat, ctx->eig_cur, d_blens, d_model,
              ctx->d_gpos, grows, gstride, d_out, epi, epi + ncb, epi + 17 * ncb,
-             e->d_epicnt, C, B, ctx->nmat, ctx->R, std::max(e->ngs, 1), e->nrootch, phy_output_len(ctx), ctx->kind};
+             e->d_epicnt, C, B, ctx->nmat, ctx->R, std::max(e->ngs, 1), e->nrootch, phy_output_len(ctx), ctx->kind,
+             flow ? e->d_fcnt : nullptr};
   hipLaunchKernelGGL(cls_epi_kernel, dim3(C * B, n), dim3(EPI_THREADS), 0, st, ea);
   *qdone = true;
   HIP_TRY(hipGetLastError());
@@ -3147,6 +3200,23 @@ int phy_create(int S, int P, int C, int rooted, int model, const uint8_t* tipcod
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess && cus > 0)
       c->cu_count = cus;
   }
+  {  // the dataflow class launch's grid: resident by construction (its items are assigned statically)
+    c->flow_pref = env_flag("PHY_FLOW", 1);
+    const int thr = C <= 4 ? 256 : 1024;
+    const void* ks[2] = {C <= 4 ? (const void*)cls_flow_kernel<256, false> : (const void*)cls_flow_kernel<1024, false>,
+                         C <= 4 ? (const void*)cls_flow_kernel<256, true> : (const void*)cls_flow_kernel<1024, true>};
+    for (int v = 0; v < 2; ++v) {
+      int nb = 0;
+      if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, ks[v], thr, 0) != hipSuccess) nb = 1;
+      // the occupancy query can over-report by one workgroup per CU (MI355X_MICROARCH.md, residency):
+      // one fewer than it says, at most 4 per CU; PHY_FLOW_WPC overrides (never above the query)
+      int wpc = std::min(4, nb >= 2 ? nb - 1 : nb);
+      const char* fw = getenv("PHY_FLOW_WPC");
+      if (fw) wpc = std::max(1, std::min(atoi(fw), std::max(nb, 1)));
+      c->flow_wgs[v] = std::max(0, wpc) * c->cu_count;
+    }
+    (void)hipGetLastError();
+  }
   // workgroup slots: an explicit budget, or up to 4 resident per CU
   c->wg_cap = (int)std::min<long>((long)c->nblk * max_draws,
                                   (long)std::max(c->wg_budget, 4 * c->cu_count) + max_draws);
@@ -3325,6 +3395,7 @@ int phy_create_multi(int S, int P, int C, int rooted, int model, const uint8_t* 
     phy_ctx* sh = nullptr;
     int rc = phy_create(S, pk, C, rooted, model, tk.data(), weights + m->p0[k], peel, max_draws, devices[k], &sh);
     if (rc) return bail(rc);
+    if (same) sh->flow_ok = false;  // same-device shards run concurrently: the flow grid could not stay resident
     m->shard.push_back(sh);
     hipEvent_t ev = nullptr;
     if (hipSetDevice(devices[k]) != hipSuccess || hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess)
@@ -3685,6 +3756,26 @@ int phy_set_engine(phy_ctx* ctx, int mode) {
   HIP_TRY(hipStreamSynchronize(ctx->stream));
   ctx->engine_pref = mode;
   return select_engine(ctx);
+}
+
+int phy_set_flow(phy_ctx* ctx, int on) {
+  if (!ctx) return fail(PHY_EINVAL, "NULL ctx");
+  if (ctx->ms) {
+    for (phy_ctx* sh : ctx->ms->shard) {
+      int rc = phy_set_flow(sh, on);
+      if (rc) return rc;
+    }
+    return PHY_OK;
+  }
+  ctx->flow_pref = on != 0;
+  ++ctx->plan_gen;
+  return PHY_OK;
+}
+
+int phy_flow(const phy_ctx* ctx) {
+  if (!ctx) return -1;
+  if (ctx->ms) return phy_flow(ctx->ms->shard[0]);
+  return (ctx->engine == 1 && flow_applies(ctx)) ? 1 : 0;
 }
 
 int phy_engine(const phy_ctx* ctx) { return ctx ? (ctx->ms ? ctx->ms->shard[0]->engine : ctx->engine) : -1; }

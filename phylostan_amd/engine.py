@@ -318,6 +318,15 @@ class TreeLikelihood:
         self.set_engine(min(med, key=med.get))
         return self.engine()
 
+    def set_flow(self, on=True):
+        """The class sweep as ONE dataflow launch (default) or one launch per
+        tree level and phase (phy_set_flow); bitwise the same results."""
+        _lib.check(self.lib.phy_set_flow(self.ctx, int(bool(on))), "phy_set_flow")
+
+    def flow(self):
+        """True when the next class-sweep launch is the dataflow one."""
+        return self.lib.phy_flow(self.ctx) == 1
+
     def engine(self):
         """The engine the next launch uses: "pattern" or "class"."""
         return ("pattern", "class")[self.lib.phy_engine(self.ctx)]

@@ -212,17 +212,31 @@ def test_config3_hcv_gtr_skyride_as_the_reference_runs_it(tmp_path, capsys):
     Stan's progress lines, an ELBO that rises and stops by tol_rel_obj, the
     skyride's `thetas.k` / `tau` columns beside `heights.k`, `rates.k`,
     `freqs.k`, and `parse` giving the .trees file `run` wrote."""
+    import argparse
     import re
+    import sys
+    import time
     from phylostan_amd import cli, stan_io
     t, a = fixture_files.write_dataset("HCV", str(tmp_path))
     script = str(tmp_path / "hcv.stan")
     assert cli.main(["build", "-m", "GTR", "-C", "4", "--clock", "strict", "--coalescent", "skyride",
                      "-s", script]) == 0
     out = str(tmp_path / "hcv")
-    capsys.readouterr()
-    cli.main(["run", "-i", a, "-t", t, "-s", script, "-o", out, "-m", "GTR", "-C", "4", "--clock", "strict",
-              "--rate", "7.9e-4", "--coalescent", "skyride", "--eta", "0.1", "--seed", "1"])
-    printed = capsys.readouterr().out
+    parser = argparse.ArgumentParser()
+    sub = parser.add_subparsers()
+    cli.create_run_parser(sub).set_defaults(func=cli.run)
+    arg = parser.parse_args(["run", "-i", a, "-t", t, "-s", script, "-o", out, "-m", "GTR", "-C", "4", "--clock",
+                             "strict", "--rate", "7.9e-4", "--coalescent", "skyride", "--eta", "0.1", "--seed", "1"])
+    lines = []
+    t0 = time.time()
+
+    def log(msg):  # the run's printed lines, echoed past pytest's capture (a long run shows progress)
+        lines.append(msg)
+        with capsys.disabled():
+            sys.stdout.write("[config3 %.1fs] %s\n" % (time.time() - t0, msg))
+            sys.stdout.flush()
+    cli.run(arg, log=log)
+    printed = "\n".join(lines)
     prog = [(int(m.group(1)), float(m.group(2))) for m in re.finditer(r"\s+(\d+)\s+(-\d+\.\d+)", printed)]
     assert len(prog) >= 5, printed[:2000]
     elbo = np.array([e for _, e in prog])

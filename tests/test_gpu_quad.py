@@ -142,3 +142,23 @@ def test_prefer_latency_engine_measures_class_against_pattern():
     name = eng.prefer_latency_engine(calls=8)
     assert set(eng.latency_probe) == {"pattern", "class"}
     assert name == min(eng.latency_probe, key=eng.latency_probe.get)
+
+
+@pytest.mark.parametrize("name", ["fluA", "many_blocks"])
+def test_quad_epilogue_handoffs_stress_bitwise(name, monkeypatch):
+    """qfin_kernel's in-launch hand-offs to the draw's last workgroup (the
+    HANDOFF note in phylo_hip.hip: write-through stores, drains, one ticket
+    add, sc1 loads) under repetition: 10,000 back-to-back 4-draw sampler
+    calls (compact rows, host buffers) in one process, every row bitwise
+    equal to the first call's -- a stale hand-off anywhere shows as a
+    differing row."""
+    case = CASES[name]()
+    n = 4
+    bl, mv = _draws(case, n, 21)
+    eng = _engine(case, max_draws=n, monkeypatch=monkeypatch)
+    eng.set_output(compact=True)
+    first = eng.evaluate_rows(bl, mv)
+    bad = 0
+    for _ in range(10000):
+        bad += int(not np.array_equal(eng.evaluate_rows(bl, mv), first))
+    assert bad == 0

@@ -1,6 +1,6 @@
 #!/bin/bash
-# Round-4 GPU session script (run through gpurun from the repository root).
-#   tools/gpu_r04.sh TAG [tests] [bench] [shard8] [synth] [multidev] [prof] [lat]
+# GPU session script (run through gpurun from the repository root).
+#   tools/gpu.sh TAG [step ...]      (steps below, run in the order given; default: tests bench shard8 synth multidev)
 # Every GPU step has its own time limit and the steps are chained: the first
 # failure ends the script (set -e), nothing is retried.  Outputs under
 # gpurun_out/TAG/.
@@ -10,48 +10,60 @@ shift
 O=gpurun_out/$TAG
 mkdir -p $O
 export TMPDIR=/tmp
-want() { [ $# -eq 0 ] && return 0; for w in "${STEPS[@]}"; do [ "$w" = "$1" ] && return 0; done; return 1; }
-STEPS=("$@")
-[ ${#STEPS[@]} -eq 0 ] && STEPS=(tests bench shard8 synth multidev)
 
-if want tests; then
+step_tests() {
   timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 240 --timeout-method thread \
     > $O/pytest.log 2>&1 || { tail -30 $O/pytest.log; exit 1; }
   tail -40 $O/pytest.log
-fi
-if want smoke; then
+}
+step_tests5() {  # this round's new GPU tests only
+  timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 800 --timeout-method thread \
+    -k "zero_rate or config3" > $O/pytest5.log 2>&1 || { tail -30 $O/pytest5.log; exit 1; }
+  tail -12 $O/pytest5.log
+}
+step_flow() {  # the dataflow class launch: bitwise against the level launches, stress, then the class suite
+  timeout -k 10 600 python -u -m pytest tests/test_gpu_class.py -x -v --timeout 240 --timeout-method thread \
+    > $O/pytest_flow.log 2>&1 || { tail -40 $O/pytest_flow.log; exit 1; }
+  tail -12 $O/pytest_flow.log
+}
+step_smoke() {
   timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1
   tail -3 $O/smoke.log
-fi
-if want bench; then
+}
+step_bench() {
   timeout -k 10 400 python bench.py --json-out $O/bench_fluA.json > $O/bench_fluA.log 2>&1
   tail -c 1500 $O/bench_fluA.json
-fi
-if want shard8; then
+}
+step_rehearse() {  # the N = 2 path of the default run on the one GPU (gloo, both ranks on device 0)
+  timeout -k 10 500 python bench.py --gpus 2 --rehearse --steps 20 --warmup 5 --json-out $O/bench_rehearse2.json \
+    > $O/bench_rehearse2.log 2>&1 || { tail -30 $O/bench_rehearse2.log; exit 1; }
+  tail -c 2500 $O/bench_rehearse2.json
+}
+step_shard8() {
   timeout -k 10 300 python bench.py --workload synthetic --shard-of 8 --steps 100 --warmup 10 \
     --no-cpu-baseline --json-out $O/bench_shard8.json > $O/bench_shard8.log 2>&1
   python -c "import json;d=json.load(open('$O/bench_shard8.json'));print('shard8', d['value'], d['ms_per_step'])"
   timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof_shard8 -o run -- \
     python bench.py --workload synthetic --shard-of 8 --steps 50 --warmup 5 --no-cpu-baseline \
     > $O/prof_shard8.log 2>&1
-fi
-if want synth; then
+}
+step_synth() {
   timeout -k 10 300 python bench.py --workload synthetic --steps 50 --warmup 5 --no-cpu-baseline \
     --json-out $O/bench_synth.json > $O/bench_synth.log 2>&1
   python -c "import json;d=json.load(open('$O/bench_synth.json'));print('synth', d['value'], d['ms_per_step'])"
   timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof_synth -o run -- \
     python bench.py --workload synthetic --steps 30 --warmup 5 --no-cpu-baseline > $O/prof_synth.log 2>&1
-fi
-if want multidev; then
+}
+step_multidev() {
   timeout -k 10 300 python bench.py --workload synthetic --multi-device 1 --steps 30 --warmup 5 \
     --no-cpu-baseline --json-out $O/bench_multidev1.json > $O/bench_multidev1.log 2>&1
   python -c "import json;d=json.load(open('$O/bench_multidev1.json'));print('multidev1', d['value'], d['config']['parallelism'])"
-fi
-if want prof; then
+}
+step_prof() {
   timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof_fluA -o run -- \
     python bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-sampler-latency > $O/prof_fluA.log 2>&1
-fi
-if want lat; then  # small calls: quad sweep against the column sweeps (PHY_QUAD=0)
+}
+step_lat() {  # small calls: quad sweep against the column sweeps (PHY_QUAD=0)
   for w in fluA HCV DS1; do
     for d in 1 4 16 32; do
       for q in 1 0; do
@@ -62,8 +74,8 @@ if want lat; then  # small calls: quad sweep against the column sweeps (PHY_QUAD
   done
   timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof_lat4 -o run -- \
     python tools/latency_probe.py --workload fluA --draws 4 --engine pattern > $O/prof_lat4.log 2>&1
-fi
-if want lat4; then  # the sampler's call only (4 draws), every engine, plus its kernel trace
+}
+step_lat4() {  # the sampler's call only (4 draws), every engine, plus its kernel trace
   for w in fluA HCV DS1; do
     for q in 1 0; do
       PHY_QUAD=$q timeout -k 10 120 python tools/latency_probe.py --workload $w --draws 4 --engine pattern \
@@ -73,15 +85,15 @@ if want lat4; then  # the sampler's call only (4 draws), every engine, plus its 
   timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof_lat4 -o run -- \
     python tools/latency_probe.py --workload fluA --draws 4 --engine pattern > $O/prof_lat4.log 2>&1
   python tools/prof_stats.py $O/prof_lat4/run_results.db
-fi
-if want sq4; then  # SQ counters of the quad sweep on the 4-draw fluA call (separate --pmc passes)
+}
+step_sq4() {  # SQ counters of the quad sweep on the 4-draw fluA call (separate --pmc passes)
   PMC_SCRIPT=tools/latency_probe.py PMC_KERNEL=qsweep timeout -k 10 600 python tools/pmc_sq.py \
     --workload fluA --draws 4 --engine pattern --calls 50 > $O/sq4_qsweep.json 2> $O/sq4_qsweep.err
   PMC_SCRIPT=tools/latency_probe.py PMC_KERNEL=qfin timeout -k 10 600 python tools/pmc_sq.py \
     --workload fluA --draws 4 --engine pattern --calls 50 > $O/sq4_qfin.json 2> $O/sq4_qfin.err
   head -c 600 $O/sq4_qsweep.json
-fi
-if want shardn; then  # the shard-of-8 evaluation with batched draws (4 NUTS chains / 8 / 16 per call)
+}
+step_shardn() {  # the shard-of-8 evaluation with batched draws (4 NUTS chains / 8 / 16 per call)
   for d in 4 8 16; do
     timeout -k 10 300 python bench.py --workload synthetic --shard-of 8 --draws $d --steps 50 --warmup 5 \
       --no-cpu-baseline --json-out $O/bench_shard8_d$d.json > $O/bench_shard8_d$d.log 2>&1
@@ -90,20 +102,20 @@ if want shardn; then  # the shard-of-8 evaluation with batched draws (4 NUTS cha
   timeout -k 10 300 python bench.py --workload synthetic --draws 4 --steps 20 --warmup 3 --no-cpu-baseline \
     --json-out $O/bench_synth_d4.json > $O/bench_synth_d4.log 2>&1
   python -c "import json;d=json.load(open('$O/bench_synth_d4.json'));print('synth draws=4', d['value'], d['ms_per_step'])"
-fi
-if want lines; then  # the committed bench lines: every dataset with its CPU baseline
+}
+step_lines() {  # the committed bench lines: every dataset with its CPU baseline
   for w in HCV DS1 synthetic; do
     timeout -k 10 500 python bench.py --workload $w --json-out $O/bench_$w.json > $O/bench_$w.log 2>&1
     python -c "import json;d=json.load(open('$O/bench_$w.json'));print('$w', d['value'], d['ms_per_step'], d['cpu_baseline']['value'])"
   done
-fi
-if want profn; then  # kernel traces of the batched-draw class sweep (4 draws per call)
+}
+step_profn() {  # kernel traces of the batched-draw class sweep (4 draws per call)
   timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof_shard8_d4 -o run -- \
     python bench.py --workload synthetic --shard-of 8 --draws 4 --steps 30 --warmup 5 --no-cpu-baseline \
     > $O/prof_shard8_d4.log 2>&1
   python tools/prof_stats.py $O/prof_shard8_d4/run_results.db | head -16
-fi
-if want pmc; then  # HBM traffic (FETCH / WRITE passes) and SQ counters of the timed kernels, fluA and synthetic
+}
+step_pmc() {  # HBM traffic (FETCH / WRITE passes) and SQ counters of the timed kernels, fluA and synthetic
   timeout -k 10 600 python tools/pmc_traffic.py --workload fluA > $O/pmc_traffic_fluA.log 2>&1 && tail -1 $O/pmc_traffic_fluA.log
   timeout -k 10 600 python tools/pmc_sq.py --steps 3 --warmup 1 --no-cpu-baseline --no-sampler-latency \
     > $O/sq_pattern_fluA.json 2> $O/sq_pattern_fluA.err && head -c 400 $O/sq_pattern_fluA.json
@@ -112,5 +124,13 @@ if want pmc; then  # HBM traffic (FETCH / WRITE passes) and SQ counters of the t
   timeout -k 10 600 python tools/pmc_sq.py --workload synthetic --engine class --steps 3 --warmup 1 --no-cpu-baseline \
     --no-sampler-latency > $O/sq_class_synthetic.json 2> $O/sq_class_synthetic.err && head -c 400 $O/sq_class_synthetic.json
   cp profiles/pmc_traffic.json profiles/sq_counters.json $O/
-fi
+}
+
+STEPS=("$@")
+[ ${#STEPS[@]} -eq 0 ] && STEPS=(tests bench shard8 synth multidev)
+for st in "${STEPS[@]}"; do
+  declare -F "step_$st" > /dev/null || { echo "unknown step $st"; exit 2; }
+  echo "== step $st ($(date +%T))"
+  "step_$st"
+done
 echo done
