@@ -295,6 +295,11 @@ struct SweepArgs {
   // qfused (fin only): the Q-parameter chain rule (qgrad_kernel's work,
   // qgrad_body) runs after the finalize, in the same workgroup
   int qfused, kind;
+  // block-waves per category (sweep_kernel): a workgroup of C x wb waves runs
+  // wb pattern blocks side by side -- wave (bw, c) is a "virtual workgroup"
+  // of its own (scratch, deep entries, dL/dP and scalar slots), sharing the
+  // workgroup's LDS matrix records, staged once (wb > 1 needs a one-chunk plan)
+  int wb;
 };
 
 // LDS carve (16-B aligned pieces), K columns per lane:
@@ -312,8 +317,9 @@ __host__ __device__ inline size_t tip_lds_bytes(int S, int K) { return tip_nib_b
 __host__ __device__ inline size_t tail_doubles(int K, int ndl) {  // per wave
   return ndl > 0 ? (size_t)ndl * K * 2 * WAVE * 2 : (size_t)K * WAVE;
 }
-__host__ __device__ inline size_t lds_bytes(int S, int C, int R, int cap_m, int K, int ndl) {
-  return tip_lds_bytes(S, K) + (size_t)C * cap_m * R * 32 + (size_t)C * tail_doubles(K, ndl) * 8;
+__host__ __device__ inline size_t lds_bytes(int S, int C, int R, int cap_m, int K, int ndl, int wb = 1) {
+  return tip_nib_bytes(S, K) * wb + 16 * 4 * sizeof(double) + (size_t)C * cap_m * R * 32 +
+         (size_t)C * wb * tail_doubles(K, ndl) * 8;
 }
 
 // Buffer resource over a workgroup's scratch / deep-stack region: loads past
@@ -681,22 +687,24 @@ __device__ void qgrad_body(const QgArgs& a, int draw, int tid, double* sh, const
 #ifndef PHY_WPE2
 #define PHY_WPE2 2  // waves per SIMD the K=2 kernel is register-budgeted for
 #endif
-template <int MAXT, int K, bool DL>
+template <int MAXT, int K, bool DL, int WB = 1>  // WB: block-waves per category (a.wb == WB)
 __global__ void __launch_bounds__(MAXT) __attribute__((amdgpu_waves_per_eu(MAXT <= 512 ? PHY_WPE2 : 4)))
     sweep_kernel(SweepArgs a, const int* __restrict__ prog) {
   extern __shared__ __attribute__((aligned(16))) unsigned char lds_raw[];
   const int lane = threadIdx.x & (WAVE - 1);
   const int C = a.C, nsteps = a.nsteps, nmat = a.nmat;
-  const int c = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int c = WB == 1 ? wv : wv % C, bw = WB == 1 ? 0 : wv / C;  // category, block-wave
   const int nthreads = blockDim.x;
   const int draw = blockIdx.y;
-  const int wg = blockIdx.y * gridDim.x + blockIdx.x;
+  // this wave's virtual workgroup: its own scratch / deep / slot regions
+  const int wg = (blockIdx.y * gridDim.x + blockIdx.x) * WB + bw;
   const int rec = a.R * 4;  // doubles per matrix record
   const int ncolwg = C * WAVE;
 
-  unsigned char* tipl = lds_raw;
-  double* mats0 = reinterpret_cast<double*>(lds_raw + tip_lds_bytes(a.S, K));
-  double* tvec = reinterpret_cast<double*>(lds_raw + tip_nib_bytes(a.S, K));  // [16][4]
+  unsigned char* tipl = lds_raw + (size_t)bw * tip_nib_bytes(a.S, K);  // this block-wave's tips
+  double* tvec = reinterpret_cast<double*>(lds_raw + tip_nib_bytes(a.S, K) * WB);  // [16][4]
+  double* mats0 = tvec + 64;
   if (threadIdx.x < 64) {  // published by the block loop's first barrier
     const unsigned b = threadIdx.x >> 2, j = threadIdx.x & 3;
     const unsigned m = b < 4 ? (1u << b) : (unsigned)(a.extra >> (4 * (b - 4))) & 15u;
@@ -747,7 +755,7 @@ __global__ void __launch_bounds__(MAXT) __attribute__((amdgpu_waves_per_eu(MAXT 
     d[ncolwg] = make_double2(v.z, v.w);
   };
   // this wave's LDS deep entries: ndl x K x 2 halves x 64 double2
-  double2* dlw = reinterpret_cast<double2*>(tail0 + (size_t)c * tstride);
+  double2* dlw = reinterpret_cast<double2*>(tail0 + (size_t)wv * tstride);
   auto dput = [&](int e, int k, const V4& v) __attribute__((always_inline)) {
     double2* d = dlw + (size_t)(e * K + k) * 2 * WAVE + lane;
     d[0] = make_double2(v.x, v.y);
@@ -774,6 +782,26 @@ __global__ void __launch_bounds__(MAXT) __attribute__((amdgpu_waves_per_eu(MAXT 
 
   // ---- this wave's chunk of matrix records in LDS (no barrier: private) ----
   int cur = -1, m0 = 0;
+  if constexpr (WB > 1) {  // one chunk holds every record; the category's block-waves stage it together, once
+    const double2* src = reinterpret_cast<const double2*>(pmat_c);
+    double2* dst = reinterpret_cast<double2*>(mats);
+    const int q2 = nmat * rec / 2;
+    for (int k0 = bw * WAVE + lane; k0 < q2; k0 += WB * WAVE * 8) {
+      double2 buf[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int k = k0 + u * WB * WAVE;
+        buf[u] = (k < q2) ? src[k] : make_double2(0.0, 0.0);
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int k = k0 + u * WB * WAVE;
+        if (k < q2) dst[k] = buf[u];
+      }
+    }
+    WAIT_VMCNT0();
+    cur = 0;  // (published by the block loop's first barrier)
+  }
   auto ensure_chunk = [&](const Step& st) {
     const int ch = st.ch;
     if (ch == cur) return;  // wave-uniform
@@ -837,28 +865,39 @@ __global__ void __launch_bounds__(MAXT) __attribute__((amdgpu_waves_per_eu(MAXT 
     }
   };
 
-  for (int blk = blockIdx.x; blk < a.nblk; blk += gridDim.x) {
+  // blocks: this wave's virtual workgroup takes blocks vg, vg + VG, ... (vg its
+  // index inside the draw, VG = gridDim.x * WB of them); every wave runs the
+  // same number of trips (the workgroup's barriers), a trip past the last
+  // block is a pass without work (the launch keeps VG <= nblk, so every
+  // virtual workgroup has at least one real block and writes its slots)
+  const int VG = gridDim.x * WB, vg = blockIdx.x * WB + bw;
+  // (one block-wave: the workgroup's own blocks, every trip real)
+  const int trips = WB == 1 ? (a.nblk - vg + VG - 1) / VG : (a.nblk + VG - 1) / VG;
+  for (int trip = 0; trip < trips; ++trip) {
+    const int blk = vg + trip * VG;
+    const bool real = WB == 1 || blk < a.nblk;  // wave-uniform
 #pragma unroll
     for (int k = 0; k < K; ++k) lofs[k] = (blk * WAVE * K + k * WAVE + lane < a.P) ? lcol[k] : OOB;
     __syncthreads();  // the previous block's tip / root-exchange reads are done
     // stage this block's tip bytes in LDS: S rows x 64K bytes, shared by the
-    // C category-waves and by both passes (8 loads in flight per thread)
-    {
+    // C category-waves of the block-wave and by both passes (8 loads in flight per thread)
+    if (real) {
       const uint32_t* src = reinterpret_cast<const uint32_t*>(a.tips);
       uint32_t* dst = reinterpret_cast<uint32_t*>(tipl);
       const int rowq = a.Ppad / 8;
       constexpr int wq = WAVE * K / 8;  // words per tip row of this block
       const int nq = a.S * wq;
-      for (int k0 = threadIdx.x; k0 < nq; k0 += nthreads * 8) {
+      const int nthr = C * WAVE, t0 = c * WAVE + lane;
+      for (int k0 = t0; k0 < nq; k0 += nthr * 8) {
         uint32_t buf[8];
 #pragma unroll
         for (int u = 0; u < 8; ++u) {
-          const int k = k0 + u * nthreads;
+          const int k = k0 + u * nthr;
           buf[u] = (k < nq) ? src[(size_t)(k / wq) * rowq + blk * wq + (k % wq)] : 0u;
         }
 #pragma unroll
         for (int u = 0; u < 8; ++u) {
-          const int k = k0 + u * nthreads;
+          const int k = k0 + u * nthr;
           if (k < nq) dst[k] = buf[u];
         }
       }
@@ -940,7 +979,7 @@ __global__ void __launch_bounds__(MAXT) __attribute__((amdgpu_waves_per_eu(MAXT 
         for (int k = 0; k < K; ++k) proot[k] = pv[k];                                                                 \
       }                                                                                                               \
     } while (0)
-    {
+    if (real) {
       V4 dA[K], dB[K];
 #pragma unroll
       for (int k = 0; k < K; ++k) dA[k] = {0.0, 0.0, 0.0, 0.0};  // step 0 has no internal child
@@ -954,20 +993,22 @@ __global__ void __launch_bounds__(MAXT) __attribute__((amdgpu_waves_per_eu(MAXT 
     }
 
     // ------------------------- root / site log L -------------------------
+    // (the C category waves of this block-wave exchange through their tails)
     double fp[K];
 #pragma unroll
     for (int k = 0; k < K; ++k) {
       fp[k] = vdot(pi, proot[k]);  // pi . p_root,c
-      tail0[(size_t)c * tstride + k * WAVE + lane] = ps_c * fp[k];
+      tail0[(size_t)wv * tstride + k * WAVE + lane] = ps_c * fp[k];
     }
     __syncthreads();
     double L[K];
 #pragma unroll
     for (int k = 0; k < K; ++k) {
       L[k] = 0.0;
-      for (int cc = 0; cc < C; ++cc) L[k] += tail0[(size_t)cc * tstride + k * WAVE + lane];
+      for (int cc = 0; cc < C; ++cc) L[k] += tail0[(size_t)(bw * C + cc) * tstride + k * WAVE + lane];
     }
     __syncthreads();  // every wave has read the exchange before deep entries are rewritten
+    if (!real) continue;  // (a trip without a block: no columns, no reverse)
     V4 topr[K];
 #pragma unroll
     for (int k = 0; k < K; ++k) {
@@ -1195,11 +1236,12 @@ __global__ void __launch_bounds__(MAXT) __attribute__((amdgpu_waves_per_eu(MAXT 
     // a release fence here would write back the whole L2 per workgroup.
     WAIT_VMCNT0();
     // fin: the finalize runs here; its LDS (inner products [C][B], then the
-    // waves' scalar partials [C][8], then qgrad's) reuses the sweep's, once
-    // every wave is done
+    // waves' scalar partials [WB][C][8], then qgrad's) reuses the sweep's,
+    // once every wave is done.  With WB block-waves the category's dL/dP is
+    // the sum of their WB slots, in block-wave order (read after the barrier)
     double* innerL = mats0;
     double* scalL = mats0 + (size_t)C * a.B;
-    if (a.fin) __syncthreads();
+    if (a.fin || WB > 1) __syncthreads();
     const double* Qd = a.eig + (size_t)draw * EIG_LEN + EIG_Q;
     double* gout = a.grows + (size_t)draw * a.grows_stride;
     double* inner_d = a.inner + (size_t)draw * C * a.B;
@@ -1209,15 +1251,19 @@ __global__ void __launch_bounds__(MAXT) __attribute__((amdgpu_waves_per_eu(MAXT 
     const double q0 = Qd[j * 4 + 0], q1 = Qd[j * 4 + 1], q2 = Qd[j * 4 + 2], q3 = Qd[j * 4 + 3];
     const int tot = nmat * 16;  // a multiple of 16: 16-lane groups are whole
     constexpr int U = PHY_EPI_U;
-    for (int k0 = lane; k0 < tot; k0 += WAVE * U) {
+    const size_t vstride = (size_t)C * nmat * 16;            // one virtual workgroup's slots
+    const double* gs0 = gs - (size_t)bw * vstride;           // block-wave 0's slot of category c
+    for (int k0 = bw * WAVE + lane; k0 < tot; k0 += WB * WAVE * U) {
       double g[U], qp[U];
       int bb[U];
 #pragma unroll
       for (int u = 0; u < U; ++u) {  // all loads in flight before any use
-        const int k = k0 + u * WAVE;
+        const int k = k0 + u * WB * WAVE;
         const int kc = k < tot ? k : lane;
         const int mm = kc >> 4;
-        g[u] = __hip_atomic_load(gs + kc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        g[u] = __hip_atomic_load(gs0 + kc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        for (int v = 1; v < WB; ++v)
+          g[u] += __hip_atomic_load(gs0 + v * vstride + kc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         const double2* col = reinterpret_cast<const double2*>(pmat_c + (size_t)mm * rec + kk * 4);  // column kk of P
         const double2 c01 = col[0], c23 = col[1];
         qp[u] = fma(q3, c23.y, fma(q2, c23.x, fma(q1, c01.y, q0 * c01.x)));
@@ -1225,7 +1271,7 @@ __global__ void __launch_bounds__(MAXT) __attribute__((amdgpu_waves_per_eu(MAXT 
       }
 #pragma unroll
       for (int u = 0; u < U; ++u) {
-        const int k = k0 + u * WAVE;
+        const int k = k0 + u * WB * WAVE;
         if (k < tot) {
           double sv = g[u] * qp[u];
           sv += __shfl_xor(sv, 8, 16);
@@ -1242,7 +1288,7 @@ __global__ void __launch_bounds__(MAXT) __attribute__((amdgpu_waves_per_eu(MAXT 
     }
     if (a.fin) {
       if (lane == 0) {
-        double* sl = scalL + (size_t)c * 8;
+        double* sl = scalL + (size_t)wv * 8;
         sl[0] = acc_ll;
         sl[1] = acc_dps;
         sl[2] = acc_f.x;
@@ -1267,7 +1313,11 @@ __global__ void __launch_bounds__(MAXT) __attribute__((amdgpu_waves_per_eu(MAXT 
         out[1 + B + cc] = sacc;
       }
       if (threadIdx.x == 0) {
-        auto tot8 = [&](int cc, int jj) { return scalL[(size_t)cc * 8 + jj]; };
+        auto tot8 = [&](int cc, int jj) {  // over the block-waves in order
+          double t = scalL[(size_t)cc * 8 + jj];
+          for (int v = 1; v < WB; ++v) t += scalL[(size_t)(v * C + cc) * 8 + jj];
+          return t;
+        };
         const double ll = tot8(0, 0);
         out[0] = isfinite(ll) ? ll : -INFINITY;
         for (int cc = 0; cc < C; ++cc) out[1 + B + C + cc] = tot8(cc, 1);
@@ -1278,7 +1328,7 @@ __global__ void __launch_bounds__(MAXT) __attribute__((amdgpu_waves_per_eu(MAXT 
         }
       }
       if (a.qfused) {  // the Q-parameter chain rule (qgrad_kernel's work, same bits)
-        double* qsh = scalL + (size_t)C * 8;
+        double* qsh = scalL + (size_t)C * 8 * WB;
         const QgArgs q{a.eig, a.model, a.blens, a.grows, a.grows_stride, a.out, a.outlen, C, B, a.kind};
         __syncthreads();  // dL/dP rows and the root term visible to the workgroup
         qgrad_body(q, draw, threadIdx.x, qsh);
@@ -2149,6 +2199,8 @@ struct phy_ctx {
   int wg_budget, cols_pref, wg_cap, lds_budget;
   int cu_count = 256, wg_resident = 512;  // resident workgroups of the current plan
   int K = 1;                   // columns per lane of the current plan
+  int wb = 1;                  // block-waves per category of the current plan (sweep_kernel's wb)
+  bool wb_pref = true;         // PHY_WB=0: one block-wave (the pre-round-5 plan)
   bool klat = false;           // K = 1 latency plan (sweep_kernel<512, 1, .>: no register spills)
   bool klat_pref = true;       // PHY_KLAT=0: the latency plan keeps the four-wave K = 1 kernel
   bool eig_fuse_pref = true;   // PHY_EIG_FUSE=0: small device batches take eig_kernel + pmat_kernel<false>
@@ -2176,7 +2228,7 @@ struct phy_ctx {
   int engine = 0, engine_pref = 0;
   ClassEngine* ce = nullptr;
   // the class sweep as one dataflow launch (cls_flow_kernel) instead of level
-  // launches: PHY_FLOW=0 / phy_set_flow(ctx, 0) turn it off; off for the
+  // launches: opt-in (PHY_FLOW=1 / phy_set_flow(ctx, 1)); never for the
   // shards of a same-device multi context (their launches run concurrently,
   // and the flow grid must be resident); flow_wgs = its resident grid
   bool flow_pref = true, flow_ok = true;
@@ -2475,7 +2527,8 @@ int nblk_for(int P, int K) { return (P + WAVE * K - 1) / (WAVE * K); }
 // workgroups, 128 VGPRs: spills) for wide launches with C > 8, and the
 // sampler's latency plan (a few draws: at most one wave per SIMD is busy)
 // at 256 VGPRs without spills (lat).
-const void* sweep_kernel_ptr(int K, bool dl, bool lat) {
+const void* sweep_kernel_ptr(int K, bool dl, bool lat, int wb = 1) {
+  if (K == 2 && wb == 2) return (const void*)sweep_kernel<512, 2, true, 2>;  // (the block-wave plan keeps the deep stack in LDS)
   if (K == 2) return dl ? (const void*)sweep_kernel<512, 2, true> : (const void*)sweep_kernel<512, 2, false>;
   if (lat) return dl ? (const void*)sweep_kernel<512, 1, true> : (const void*)sweep_kernel<512, 1, false>;
   return dl ? (const void*)sweep_kernel<1024, 1, true> : (const void*)sweep_kernel<1024, 1, false>;
@@ -2546,18 +2599,33 @@ int plan_chunks(phy_ctx* c) {
     for (int t = by_waves; t >= 1; --t)
       if (place(LDS_CAP / t, t == 1)) break;
   }
-  const size_t lds = lds_bytes(c->S, c->C, c->R, cap, K, ndl);
+  // Block-waves (the batched two-column plan): a workgroup of C x wb waves --
+  // wb pattern blocks side by side, two waves per SIMD as before -- whose LDS
+  // holds EVERY matrix record of the draw (one chunk, staged once per
+  // workgroup instead of once per chunk per block) and the whole deep stack;
+  // taken when it fits one workgroup per CU (fluA: 2 x 4 waves, 159 KB)
+  int wb = 1;
+  if (K == 2 && !lat && c->wb_pref && c->lds_budget == 0 && c->deep_pref != 2 && c->C <= 4) {
+    const int w = std::min(2, nb);  // (sweep_kernel's WB instantiations: 1, 2)
+    if (w >= 2 && lds_bytes(c->S, c->C, c->R, c->nmat, K, c->ndeep, w) <= LDS_CAP) {
+      wb = w;
+      cap = c->nmat;
+      ndl = c->ndeep;
+    }
+  }
+  const size_t lds = lds_bytes(c->S, c->C, c->R, cap, K, ndl, wb);
   if (lds > LDS_CAP) return fail(PHY_EINVAL, "tree too large for LDS (tips of one block)");
   c->K = K;
+  c->wb = wb;
   c->klat = lat;
   c->nblk = nb;
   ++c->plan_gen;
-  c->wg_resident = c->cu_count * std::min<int>(by_waves, (int)(LDS_CAP / lds));
+  c->wg_resident = wb > 1 ? c->cu_count : c->cu_count * std::min<int>(by_waves, (int)(LDS_CAP / lds));
   {
     // workgroup regions the largest launch of this plan may use
     // (launch_pattern's gx per draw), grown here so no launch fails
     const long budget = c->wg_budget > 0 ? c->wg_budget : c->wg_resident;
-    const long need = std::min<long>((long)c->max_draws * nb, budget + c->max_draws);
+    const long need = std::min<long>((long)c->max_draws * nb, (budget + c->max_draws) * wb);  // virtual workgroups
     if (need > c->wg_cap) {
       HIP_TRY(hipStreamSynchronize(c->stream));
       int rc = alloc_wg_buffers(c, need);
@@ -2706,12 +2774,32 @@ int launch_class(phy_ctx* ctx, int n, const double* d_blens, const double* d_mod
   }
   if (ctx->timing && (rc = timing_begin(ctx, st, &e0, &e1))) return rc;
   if (flow) {
-    const FlowArgs fa{e->d_items, e->nitems, n, e->d_fcnt + 4, e->ncnt, e->d_fcnt};
+    unsigned long long* trace = nullptr;
+    const char* tpath = getenv("PHY_FLOW_TRACE");  // diagnostics: per-item wall-clock trace appended to this file
+    if (tpath && *tpath) HIP_TRY(hipMallocAsync((void**)&trace, sizeof(unsigned long long) * 4 * e->nitems * n, st));
+    const FlowArgs fa{e->d_items, e->nitems, n, e->d_fcnt + 4, e->ncnt, e->d_fcnt, trace};
     const long long total = (long long)e->nitems * n;
+    if (total >= (1ll << 31)) return fail(PHY_ERANGE, "class sweep: too many dataflow items x draws");
     const int grid = (int)std::min<long long>(total, (long long)ctx->flow_wgs[e->root_tips ? 1 : 0]);
     auto fk = C <= 4 ? (e->root_tips ? cls_flow_kernel<256, true> : cls_flow_kernel<256, false>)
                      : (e->root_tips ? cls_flow_kernel<1024, true> : cls_flow_kernel<1024, false>);
     hipLaunchKernelGGL(fk, dim3(std::max(grid, 1)), dim3(C * WAVE), 0, st, a, fa);
+    if (trace) {  // items (kind, idx, level-free), then the trace rows; one record per launch
+      const size_t nt = (size_t)4 * e->nitems * n;
+      std::vector<unsigned long long> h(nt);
+      std::vector<FItem> hi(e->nitems);
+      HIP_TRY(hipMemcpyAsync(h.data(), trace, nt * sizeof(unsigned long long), hipMemcpyDeviceToHost, st));
+      HIP_TRY(hipMemcpyAsync(hi.data(), e->d_items, hi.size() * sizeof(FItem), hipMemcpyDeviceToHost, st));
+      HIP_TRY(hipStreamSynchronize(st));
+      HIP_TRY(hipFree(trace));
+      if (FILE* fp = fopen(tpath, "ab")) {
+        const int hdr[4] = {e->nitems, n, grid, (int)sizeof(FItem)};
+        fwrite(hdr, sizeof(int), 4, fp);
+        fwrite(hi.data(), sizeof(FItem), hi.size(), fp);
+        fwrite(h.data(), sizeof(unsigned long long), nt, fp);
+        fclose(fp);
+      }
+    }
   }
   if (!flow && e->Lc > 0)  // levels 1..Lc: one workgroup per (bottom clade, dc)
     hipLaunchKernelGGL(cls_clade_fwd_kernel, dim3(e->nclade, dcn), dim3(CLADE_THREADS), 0, st, a,
@@ -2949,7 +3037,7 @@ int launch_quad(phy_ctx* ctx, int n, const double* d_blens, const double* d_mode
                    ctx->d_gslot, ctx->d_sslot, d_site,       d_out,        ctx->d_mat_branch, ctx->eig_cur,
                    ctx->d_inner, ctx->S,       ctx->P,       ctx->Ppad,    C,              ctx->nsteps,
                    ctx->nslots,  ctx->ndeep,   0,            ctx->nblk,    ctx->nmat,    ctx->R,         ctx->nmat,
-                   B,            phy_output_len(ctx), 0, ctx->extra, 0, d_blens, grows, gstride, 0, ctx->kind};
+                   B,            phy_output_len(ctx), 0, ctx->extra, 0, d_blens, grows, gstride, 0, ctx->kind, 1};
   qa.qscr = ctx->d_qscr;
   qa.nblk = nb;
   qa.pmat_out = ctx->d_pmat;
@@ -2996,28 +3084,31 @@ int launch_pattern(phy_ctx* ctx, int n, const double* d_blens, const double* d_m
     return launch_quad(ctx, n, d_blens, d_model, d_out, d_site, st, grows, gstride, qdone);
   // persistent workgroups: the explicit budget, else exactly what is resident
   const int budget = ctx->wg_budget > 0 ? ctx->wg_budget : ctx->wg_resident;
-  const int gx = std::max(1, std::min(ctx->nblk, (budget + n - 1) / n));
-  if ((size_t)gx * n > (size_t)ctx->wg_cap) return fail(PHY_ERANGE, "workgroup cap exceeded");
-  const size_t lds = lds_bytes(ctx->S, C, ctx->R, ctx->cap_m, ctx->K, ctx->ndl);
+  // block-waves of this launch: at most one per block, so every virtual
+  // workgroup (gx x wb of them per draw, <= nblk) has a block to write its slots
+  const int wb = std::max(1, std::min(ctx->wb, ctx->nblk));
+  const int gx = std::max(1, std::min(ctx->nblk / wb, (budget + n - 1) / n));
+  if ((size_t)gx * wb * n > (size_t)ctx->wg_cap) return fail(PHY_ERANGE, "workgroup cap exceeded");
+  const size_t lds = lds_bytes(ctx->S, C, ctx->R, ctx->cap_m, ctx->K, ctx->ndl, wb);
   const int g_direct = (gx == 1) ? 1 : 0;
-  // finalize inside the sweep when its LDS holds [C][B] + [C][8] doubles
+  // finalize inside the sweep when its LDS holds [C][B] + [wb][C][8] doubles
   // past the tips; the chain rule too when QG_SHARED more fit
-  const size_t room = lds - tip_lds_bytes(ctx->S, ctx->K);
-  const int fin = (g_direct && ctx->fin_pref && ((size_t)C * B + 8 * C) * 8 <= room) ? 1 : 0;
-  const int qf = (fin && ctx->qfuse_pref && ((size_t)C * B + 8 * C + QG_SHARED) * 8 <= room) ? 1 : 0;
+  const size_t room = lds - tip_nib_bytes(ctx->S, ctx->K) * wb - 16 * 4 * sizeof(double);
+  const int fin = (g_direct && ctx->fin_pref && ((size_t)C * B + 8 * C * wb) * 8 <= room) ? 1 : 0;
+  const int qf = (fin && ctx->qfuse_pref && ((size_t)C * B + 8 * C * wb + QG_SHARED) * 8 <= room) ? 1 : 0;
   SweepArgs sa{ctx->d_tips,  ctx->d_w,     ctx->d_pmat,  d_model,      ctx->d_scratch, ctx->d_dstk,
                ctx->d_gslot, ctx->d_sslot, d_site,       d_out,        ctx->d_mat_branch, ctx->eig_cur,
                ctx->d_inner, ctx->S,       ctx->P,       ctx->Ppad,    C,              ctx->nsteps,
                ctx->nslots,  ctx->ndeep,   ctx->ndl,     ctx->nblk,    ctx->nmat,    ctx->R,         ctx->cap_m,
                B,            phy_output_len(ctx), g_direct, ctx->extra, fin, d_blens, grows, gstride,
-               qf,           ctx->kind};
+               qf,           ctx->kind,      wb};
   hipEvent_t e0 = nullptr, e1 = nullptr;
   if (ctx->timing) {
     int rc = timing_begin(ctx, st, &e0, &e1);
     if (rc) return rc;
   }
-  const int threads = C * WAVE;
-  const void* kern = sweep_kernel_ptr(ctx->K, ctx->deep_lds, ctx->klat);
+  const int threads = C * WAVE * wb;
+  const void* kern = sweep_kernel_ptr(ctx->K, ctx->deep_lds, ctx->klat, wb);
   {
     const int* prog = ctx->d_prog;
     void* kargs[] = {(void*)&sa, (void*)&prog};
@@ -3028,9 +3119,9 @@ int launch_pattern(phy_ctx* ctx, int n, const double* d_blens, const double* d_m
   // a draw over a few workgroups: the finalize sums their slots itself
   // (one epilogue launch: slot sums, finalize, chain rule); over many, the
   // wide gsum kernel first
-  const int gsum_in = (!g_direct && gx <= 16) ? 1 : 0;
+  const int gsum_in = (!g_direct && gx * wb <= 16) ? 1 : 0;
   FinArgs fa{ctx->d_gslot, ctx->d_sslot, ctx->d_pmat, ctx->eig_cur, d_blens, d_model, ctx->d_gpos, ctx->d_inner, d_out,
-             C,            B,            ctx->nmat,   gx,          phy_output_len(ctx), g_direct, ctx->R, grows, gstride,
+             C,            B,            ctx->nmat,   gx * wb,     phy_output_len(ctx), g_direct, ctx->R, grows, gstride,
              ctx->kind,    gsum_in,      (!fin && ctx->qfuse_pref) ? 1 : 0};
   if (!g_direct && !gsum_in) {
     hipLaunchKernelGGL(gsum_kernel, dim3((C * B * 16 + 63) / 64, n), dim3(256), 0, st, fa);
@@ -3188,6 +3279,7 @@ int phy_create(int S, int P, int C, int rooted, int model, const uint8_t* tipcod
     c->eig_fuse_pref = env_flag("PHY_EIG_FUSE", 1);
     const char* qk2 = getenv("PHY_QUAD");
     c->quad_pref = qk2 ? atoi(qk2) != 0 : true;
+    c->wb_pref = env_flag("PHY_WB", 1);
 
   }
   hipError_t he = hipSetDevice(device);
@@ -3201,7 +3293,7 @@ int phy_create(int S, int P, int C, int rooted, int model, const uint8_t* tipcod
       c->cu_count = cus;
   }
   {  // the dataflow class launch's grid: resident by construction (its items are assigned statically)
-    c->flow_pref = env_flag("PHY_FLOW", 1);
+    c->flow_pref = env_flag("PHY_FLOW", 0);  // opt-in: measured slower than the level launches
     const int thr = C <= 4 ? 256 : 1024;
     const void* ks[2] = {C <= 4 ? (const void*)cls_flow_kernel<256, false> : (const void*)cls_flow_kernel<1024, false>,
                          C <= 4 ? (const void*)cls_flow_kernel<256, true> : (const void*)cls_flow_kernel<1024, true>};
@@ -3226,6 +3318,8 @@ int phy_create(int S, int P, int C, int rooted, int model, const uint8_t* tipcod
     for (int k = 0; k < 8; ++k)
       (void)hipFuncSetAttribute(sweep_kernel_ptr(1 + (k & 1), (k >> 1) & 1, (k >> 2) & 1),
                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)LDS_CAP);
+    (void)hipFuncSetAttribute(sweep_kernel_ptr(2, true, false, 2), hipFuncAttributeMaxDynamicSharedMemorySize,
+                              (int)LDS_CAP);
     (void)hipFuncSetAttribute((const void*)finalize_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)LDS_CAP);
     for (const void* kern : {(const void*)qsweep_kernel<256>, (const void*)qsweep_kernel<1024>}) {
       hipFuncAttributes fa{};  // its static eigensystem copy counts against the cap too
@@ -3816,7 +3910,7 @@ int phy_lds_plan(const phy_ctx* ctx, int* n_chunks, int* matrices_per_chunk, int
   if (n_chunks) *n_chunks = ctx->nchunks;  // matrix-record chunks per pass
   if (matrices_per_chunk) *matrices_per_chunk = ctx->cap_m;
   if (lds_bytes_out)
-    *lds_bytes_out = (int)lds_bytes(ctx->S, ctx->C, ctx->R, ctx->cap_m, ctx->K, ctx->ndl);
+    *lds_bytes_out = (int)lds_bytes(ctx->S, ctx->C, ctx->R, ctx->cap_m, ctx->K, ctx->ndl, ctx->wb);
   return PHY_OK;
 }
 

@@ -319,8 +319,9 @@ class TreeLikelihood:
         return self.engine()
 
     def set_flow(self, on=True):
-        """The class sweep as ONE dataflow launch (default) or one launch per
-        tree level and phase (phy_set_flow); bitwise the same results."""
+        """The class sweep as ONE dataflow launch (opt-in) or one launch per
+        tree level and phase (default, measured faster); phy_set_flow;
+        bitwise the same results."""
         _lib.check(self.lib.phy_set_flow(self.ctx, int(bool(on))), "phy_set_flow")
 
     def flow(self):

@@ -166,6 +166,8 @@ def test_class_clades_repetitive_alignment_bitwise():
 
 def _flow_pair(case, max_draws=1):
     eng = _class_engine(case, max_draws=max_draws)
+    assert not eng.flow()  # opt-in
+    eng.set_flow(True)
     assert eng.flow()
     lvl = _class_engine(case, max_draws=max_draws)
     lvl.set_flow(False)
@@ -233,16 +235,20 @@ def test_class_flow_stress_bitwise_over_many_calls():
     bl = torch.tensor(np.stack([case.blens, case.blens * 1.1]), device=dev)
     mv = torch.tensor(np.stack([case.model_vec()] * 2), device=dev)
     out = torch.zeros((2, eng.outlen), dtype=torch.float64, device=dev)
-    st = torch.cuda.current_stream(dev).cuda_stream  # the engine's launches and torch's compares in one order
-    eng.evaluate_device(bl.data_ptr(), mv.data_ptr(), out.data_ptr(), n_draws=2, stream=st)
-    first = out.clone()
-    ref = torch.zeros_like(out)
-    lvl.evaluate_device(bl.data_ptr(), mv.data_ptr(), ref.data_ptr(), n_draws=2, stream=st)
     torch.cuda.synchronize()
-    assert torch.equal(first, ref)
-    bad = torch.zeros((), dtype=torch.int64, device=dev)
-    for _ in range(10000):
+    stream = torch.cuda.Stream(dev)  # a real stream: the engine's launches and torch's compares in one order
+    st = stream.cuda_stream          # (torch's default stream is handle 0, which the engine reads as "its own")
+    with torch.cuda.stream(stream):
         eng.evaluate_device(bl.data_ptr(), mv.data_ptr(), out.data_ptr(), n_draws=2, stream=st)
-        bad += (out != first).any().to(torch.int64)
-    torch.cuda.synchronize()
+        first = out.clone()
+        ref = torch.zeros_like(out)
+        lvl.evaluate_device(bl.data_ptr(), mv.data_ptr(), ref.data_ptr(), n_draws=2, stream=st)
+        stream.synchronize()
+        assert np.isfinite(first.cpu().numpy()).all() and first[0, 0].item() < 0.0
+        assert torch.equal(first, ref)
+        bad = torch.zeros((), dtype=torch.int64, device=dev)
+        for _ in range(10000):
+            eng.evaluate_device(bl.data_ptr(), mv.data_ptr(), out.data_ptr(), n_draws=2, stream=st)
+            bad += (out != first).any().to(torch.int64)
+        stream.synchronize()
     assert int(bad.item()) == 0

@@ -252,7 +252,9 @@ def test_config3_hcv_gtr_skyride_as_the_reference_runs_it(tmp_path, capsys):
     assert data.shape == (1001, len(header)) and np.isfinite(data).all()
     tau = data[:, header.index("tau")]
     assert np.all(tau > 0)
-    cli.main(["parse", "--samples", out, "-t", t, "-o", str(tmp_path / "parsed.trees")])
+    # parse with the run's fixed rate (phylostan.py parse --rate): the same .trees run wrote
+    cli.main(["parse", "--samples", out, "-t", t, "--rate", "7.9e-4", "-o", str(tmp_path / "parsed.trees")])
     ran = open(out + ".trees").read()
     parsed = open(str(tmp_path / "parsed.trees")).read()
-    assert ran.count("tree ") == 1001 and ran == parsed
+    assert ran.count("tree ") == 1001
+    assert ran == parsed, "parse's .trees differ from run's"  # (no diff of two multi-MB strings in the report)

@@ -39,6 +39,40 @@ step_rehearse() {  # the N = 2 path of the default run on the one GPU (gloo, bot
     > $O/bench_rehearse2.log 2>&1 || { tail -30 $O/bench_rehearse2.log; exit 1; }
   tail -c 2500 $O/bench_rehearse2.json
 }
+step_flowtrace() {  # the dataflow class launch's per-item trace (shard of 8, one GPU), and the level launches beside it
+  rm -f $O/ft.bin
+  PHY_FLOW_TRACE=$O/ft.bin timeout -k 10 300 python bench.py --workload synthetic --shard-of 8 --steps 3 --warmup 1 \
+    --no-cpu-baseline --json-out $O/bench_ft.json > $O/bench_ft.log 2>&1
+  python tools/flow_trace.py $O/ft.bin
+  for w in 3 4; do
+    PHY_FLOW_WPC=$w timeout -k 10 300 python bench.py --workload synthetic --shard-of 8 --steps 100 --warmup 10 \
+      --no-cpu-baseline --json-out $O/bench_shard8_w$w.json > $O/bench_shard8_w$w.log 2>&1
+    python -c "import json;d=json.load(open('$O/bench_shard8_w$w.json'));print('shard8 flow wpc $w', d['value'], d['ms_per_step'])"
+  done
+  PHY_FLOW=0 timeout -k 10 300 python bench.py --workload synthetic --shard-of 8 --steps 100 --warmup 10 \
+    --no-cpu-baseline --json-out $O/bench_shard8_lvl.json > $O/bench_shard8_lvl.log 2>&1
+  python -c "import json;d=json.load(open('$O/bench_shard8_lvl.json'));print('shard8 level launches', d['value'], d['ms_per_step'])"
+}
+step_cfg3dbg() {  # config 3 alone, with a stack dump if it hangs
+  timeout -k 10 300 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread \
+    -k "config3" > $O/pytest_cfg3.log 2>&1 || { tail -80 $O/pytest_cfg3.log; exit 1; }
+  tail -5 $O/pytest_cfg3.log
+}
+step_wbab() {  # block-wave plan (PHY_WB, default on) against the one-block-wave plan, alternating, fluA batched
+  for r in 1 2; do
+    for w in 1 0; do
+      PHY_WB=$w timeout -k 10 200 python bench.py --steps 100 --warmup 10 --no-cpu-baseline --no-sampler-latency \
+        --no-synthetic --json-out $O/bench_wb${w}_$r.json > $O/bench_wb${w}_$r.log 2>&1
+      python -c "import json;d=json.load(open('$O/bench_wb${w}_$r.json'));print('PHY_WB=$w', d['value'], d['roofline']['kernel_avg_ms'], d['program'])"
+    done
+  done
+}
+step_parity() {  # the parity suites of the pattern sweep (every plan) and the configs
+  timeout -k 10 600 python -u -m pytest tests/test_gpu_00_configs.py tests/test_gpu_parity.py tests/test_gpu_large_cb.py \
+    -x -q --timeout 240 --timeout-method thread -k "not synthetic_full_size and not config5" \
+    > $O/pytest_parity.log 2>&1 || { tail -40 $O/pytest_parity.log; exit 1; }
+  tail -15 $O/pytest_parity.log
+}
 step_shard8() {
   timeout -k 10 300 python bench.py --workload synthetic --shard-of 8 --steps 100 --warmup 10 \
     --no-cpu-baseline --json-out $O/bench_shard8.json > $O/bench_shard8.log 2>&1
