@@ -2200,7 +2200,7 @@ struct phy_ctx {
   int cu_count = 256, wg_resident = 512;  // resident workgroups of the current plan
   int K = 1;                   // columns per lane of the current plan
   int wb = 1;                  // block-waves per category of the current plan (sweep_kernel's wb)
-  bool wb_pref = true;         // PHY_WB=0: one block-wave (the pre-round-5 plan)
+  bool wb_pref = false;        // PHY_WB=1: two block-waves per category when one chunk fits (opt-in, slower)
   bool klat = false;           // K = 1 latency plan (sweep_kernel<512, 1, .>: no register spills)
   bool klat_pref = true;       // PHY_KLAT=0: the latency plan keeps the four-wave K = 1 kernel
   bool eig_fuse_pref = true;   // PHY_EIG_FUSE=0: small device batches take eig_kernel + pmat_kernel<false>
@@ -3279,7 +3279,7 @@ int phy_create(int S, int P, int C, int rooted, int model, const uint8_t* tipcod
     c->eig_fuse_pref = env_flag("PHY_EIG_FUSE", 1);
     const char* qk2 = getenv("PHY_QUAD");
     c->quad_pref = qk2 ? atoi(qk2) != 0 : true;
-    c->wb_pref = env_flag("PHY_WB", 1);
+    c->wb_pref = env_flag("PHY_WB", 0);  // opt-in: measured slower
 
   }
   hipError_t he = hipSetDevice(device);

@@ -484,3 +484,28 @@ def test_retired_resident_engine_is_refused():
     with pytest.raises(PhyloHipError, match="retired"):
         eng.set_engine(3)
     assert eng.engine() == "pattern"
+
+
+def test_block_wave_plan_rows_bitwise_equal(monkeypatch):
+    """The opt-in block-wave plan (PHY_WB=1: a workgroup of C x 2 waves runs
+    two pattern blocks over one LDS chunk holding every matrix record) forms
+    the same sums in the same order as the default plan -- the second
+    block's dL/dP added to the first's (slot sum instead of atomic add), the
+    rebuilt cherries the same arithmetic as stored ones -- so every output
+    row of a 256-draw fluA launch is bitwise the default plan's."""
+    from phylostan_amd import models
+    from phylostan_amd.engine import TreeLikelihood
+    base = cases.fluA_case()
+    n = 256
+    rng = np.random.default_rng(29)
+    blens = base.blens[None, :] * rng.uniform(0.6, 1.4, (n, base.blens.size))
+    mvs = np.stack([models.model_vector(base.freqs, models.hky_exchangeabilities(rng.uniform(3.0, 8.0)), base.rs,
+                                        base.ps) for _ in range(n)])
+    rows = {}
+    for wb in ("0", "1"):
+        monkeypatch.setenv("PHY_WB", wb)
+        eng = TreeLikelihood(base.tipcodes, base.weights, base.peel0, True, "HKY", 4, max_draws=n)
+        plan = eng.lds_plan()
+        assert plan["n_chunks"] == (1 if wb == "1" else 2), plan
+        rows[wb] = eng.evaluate_rows(blens, mvs)
+    assert np.array_equal(rows["0"], rows["1"])

@@ -41,11 +41,11 @@ step_rehearse() {  # the N = 2 path of the default run on the one GPU (gloo, bot
 }
 step_flowtrace() {  # the dataflow class launch's per-item trace (shard of 8, one GPU), and the level launches beside it
   rm -f $O/ft.bin
-  PHY_FLOW_TRACE=$O/ft.bin timeout -k 10 300 python bench.py --workload synthetic --shard-of 8 --steps 3 --warmup 1 \
+  PHY_FLOW=1 PHY_FLOW_TRACE=$O/ft.bin timeout -k 10 300 python bench.py --workload synthetic --shard-of 8 --steps 3 --warmup 1 \
     --no-cpu-baseline --json-out $O/bench_ft.json > $O/bench_ft.log 2>&1
   python tools/flow_trace.py $O/ft.bin
   for w in 3 4; do
-    PHY_FLOW_WPC=$w timeout -k 10 300 python bench.py --workload synthetic --shard-of 8 --steps 100 --warmup 10 \
+    PHY_FLOW=1 PHY_FLOW_WPC=$w timeout -k 10 300 python bench.py --workload synthetic --shard-of 8 --steps 100 --warmup 10 \
       --no-cpu-baseline --json-out $O/bench_shard8_w$w.json > $O/bench_shard8_w$w.log 2>&1
     python -c "import json;d=json.load(open('$O/bench_shard8_w$w.json'));print('shard8 flow wpc $w', d['value'], d['ms_per_step'])"
   done
@@ -72,6 +72,24 @@ step_parity() {  # the parity suites of the pattern sweep (every plan) and the c
     -x -q --timeout 240 --timeout-method thread -k "not synthetic_full_size and not config5" \
     > $O/pytest_parity.log 2>&1 || { tail -40 $O/pytest_parity.log; exit 1; }
   tail -15 $O/pytest_parity.log
+}
+step_latab() {  # sampler-call latency (1 / 4 / 100 draws, fluA) of this build against variants/r03.so and r04.so, alternating
+  for d in 100 4 1; do
+    for r in 1 2; do
+      for v in base variants/r03.so variants/r04.so; do
+        if [ $v = base ]; then env=""; n=base; else env="PHYLO_HIP_AB=1 PHYLO_HIP_LIB=$PWD/$v"; n=$(basename $v .so); fi
+        env $env timeout -k 10 120 python tools/latency_probe.py --workload fluA --draws $d --engine pattern \
+          > $O/lat_${n}_${d}_$r.log 2>&1
+        echo "$n draws=$d rep$r $(tail -1 $O/lat_${n}_${d}_$r.log)"
+      done
+    done
+  done
+  for v in base variants/r03.so variants/r04.so; do  # the 100-draw call's kernels on the device clock
+    if [ $v = base ]; then env=""; n=base; else env="PHYLO_HIP_AB=1 PHYLO_HIP_LIB=$PWD/$v"; n=$(basename $v .so); fi
+    env $env timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof_lat100_$n -o run -- \
+      python tools/latency_probe.py --workload fluA --draws 100 --engine pattern > $O/prof_lat100_$n.log 2>&1
+    echo "== $n"; python tools/prof_stats.py $O/prof_lat100_$n/run_results.db | head -8
+  done
 }
 step_shard8() {
   timeout -k 10 300 python bench.py --workload synthetic --shard-of 8 --steps 100 --warmup 10 \
