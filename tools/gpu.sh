@@ -1,6 +1,13 @@
 #!/bin/bash
 # GPU session script (run through gpurun from the repository root).
 #   tools/gpu.sh TAG [step ...]      (steps below, run in the order given; default: tests bench shard8 synth multidev)
+# A/B steps read their variants from AB_VARIANTS, a space-separated list whose
+# items are `base` (this build), a variant library `variants/x.so` (loaded with
+# PHYLO_HIP_AB=1 PHYLO_HIP_LIB), or environment settings `K=V[,K=V...]` for
+# this build; they alternate the variants, two rounds (AB_REPS):
+#   AB_VARIANTS="base variants/x.so PHY_WB=1" AB_ARGS="--workload synthetic --shard-of 8" tools/gpu.sh T ab
+#   AB_VARIANTS="base variants/x.so" LAT_WLS="fluA HCV" LAT_DRAWS="4 100" tools/gpu.sh T latab
+#   tools/gpu.sh T infer | draws | ldsenv     (the round-2/3 inference, draws-per-launch and LDS-plan runs)
 # Every GPU step has its own time limit and the steps are chained: the first
 # failure ends the script (set -e), nothing is retried.  Outputs under
 # gpurun_out/TAG/.
@@ -73,22 +80,71 @@ step_parity() {  # the parity suites of the pattern sweep (every plan) and the c
     > $O/pytest_parity.log 2>&1 || { tail -40 $O/pytest_parity.log; exit 1; }
   tail -15 $O/pytest_parity.log
 }
-step_latab() {  # sampler-call latency (1 / 4 / 100 draws, fluA) of this build against variants/r03.so and r04.so, alternating
-  for d in 100 4 1; do
-    for r in 1 2; do
-      for v in base variants/r03.so variants/r04.so; do
-        if [ $v = base ]; then env=""; n=base; else env="PHYLO_HIP_AB=1 PHYLO_HIP_LIB=$PWD/$v"; n=$(basename $v .so); fi
-        env $env timeout -k 10 120 python tools/latency_probe.py --workload fluA --draws $d --engine pattern \
-          > $O/lat_${n}_${d}_$r.log 2>&1
-        echo "$n draws=$d rep$r $(tail -1 $O/lat_${n}_${d}_$r.log)"
+vname() {  # file-name tag of a variant spec
+  case $1 in base) echo base ;; *.so) basename $1 .so ;; *) echo "$1" | tr ',=/' '__-' ;; esac
+}
+vrun() {  # vrun SPEC cmd... : the command under that variant
+  local v=$1; shift
+  case $v in
+    base) "$@" ;;
+    *.so) PHYLO_HIP_AB=1 PHYLO_HIP_LIB=$PWD/$v "$@" ;;
+    *) env $(echo "$v" | tr ',' ' ') "$@" ;;
+  esac
+}
+step_ab() {  # bench.py A/B: AB_ARGS over AB_VARIANTS (see the header), alternating
+  for r in $(seq 1 ${AB_REPS:-2}); do
+    for v in ${AB_VARIANTS:-base}; do
+      n=$(vname $v)
+      vrun $v timeout -k 10 300 python bench.py ${AB_ARGS:-} --no-cpu-baseline --json-out $O/ab_${n}_$r.json \
+        > $O/ab_${n}_$r.log 2>&1 || { tail -20 $O/ab_${n}_$r.log; exit 1; }
+      python -c "import json;d=json.load(open('$O/ab_${n}_$r.json'));r=d.get('roofline',{});print('$n rep$r', d['value'], d['ms_per_step'], r.get('kernel_avg_ms'))"
+    done
+  done
+}
+step_latab() {  # sampler-call latency A/B: LAT_WLS x LAT_DRAWS over AB_VARIANTS, alternating, then a kernel trace per variant
+  local V=${AB_VARIANTS:-base variants/r03.so variants/r04.so}
+  for d in ${LAT_DRAWS:-100 4 1}; do
+    for r in $(seq 1 ${AB_REPS:-2}); do
+      for w in ${LAT_WLS:-fluA}; do
+        for v in $V; do
+          n=$(vname $v)
+          vrun $v timeout -k 10 120 python tools/latency_probe.py --workload $w --draws $d --engine pattern \
+            > $O/lat_${n}_${w}_${d}_$r.log 2>&1 || { tail -20 $O/lat_${n}_${w}_${d}_$r.log; exit 1; }
+          echo "$n $w draws=$d rep$r $(tail -1 $O/lat_${n}_${w}_${d}_$r.log)"
+        done
       done
     done
   done
-  for v in base variants/r03.so variants/r04.so; do  # the 100-draw call's kernels on the device clock
-    if [ $v = base ]; then env=""; n=base; else env="PHYLO_HIP_AB=1 PHYLO_HIP_LIB=$PWD/$v"; n=$(basename $v .so); fi
-    env $env timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof_lat100_$n -o run -- \
-      python tools/latency_probe.py --workload fluA --draws 100 --engine pattern > $O/prof_lat100_$n.log 2>&1
-    echo "== $n"; python tools/prof_stats.py $O/prof_lat100_$n/run_results.db | head -8
+  [ -n "${LAT_TRACE:-1}" ] || return 0
+  local d=${LAT_TRACE_DRAWS:-100}
+  for v in $V; do  # that call's kernels on the device clock
+    n=$(vname $v)
+    vrun $v timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof_lat${d}_$n -o run -- \
+      python tools/latency_probe.py --workload fluA --draws $d --engine pattern > $O/prof_lat${d}_$n.log 2>&1
+    echo "== $n"; python tools/prof_stats.py $O/prof_lat${d}_$n/run_results.db | head -8
+  done
+}
+step_infer() {  # the inference tests and config 5 (full NUTS on fluA, GPU gradients)
+  timeout -k 10 600 python -u -m pytest tests/test_gpu_class.py tests/test_gpu_inference.py -x -v --timeout 400 \
+    --timeout-method thread > $O/pytest_inf.log 2>&1 || { tail -30 $O/pytest_inf.log; exit 1; }
+  tail -12 $O/pytest_inf.log
+  timeout -k 10 300 python tools/run_config5.py --out $O/config5 > $O/config5.log 2>&1
+  tail -1 $O/config5.log
+}
+step_draws() {  # fluA throughput against draws per launch, alternating
+  for r in 1 2; do for n in 8192 16384 32768; do
+    timeout -k 10 200 python bench.py --draws $n --steps $((1638400 / n)) --warmup 5 --no-cpu-baseline --no-synthetic \
+      --json-out $O/d${n}_$r.json > $O/d${n}_$r.log 2>&1
+    python -c "import json;d=json.load(open('$O/d${n}_$r.json'));print('draws $n rep$r', round(d['value']), round(d['roofline']['kernel_avg_ms'],3))"
+  done; done
+}
+step_ldsenv() {  # LDS plans through the environment (one-chunk budget, deep-stack variants)
+  for e in - PHY_LDS_BUDGET=163840 PHY_LDS_BUDGET=163840,PHY_DEEP=2 PHY_DEEP=2; do
+    [ $e = - ] && v=base || v=$e
+    n=$(vname $v)
+    vrun $v timeout -k 10 200 python bench.py --no-cpu-baseline --no-synthetic --steps 100 --warmup 10 \
+      --json-out $O/lds_$n.json > $O/lds_$n.log 2>&1
+    python -c "import json;d=json.load(open('$O/lds_$n.json'));p=d['program'];print('$n', round(d['value']), round(d['roofline']['kernel_avg_ms'],3), p['n_chunks'], p['matrices_per_chunk'], p['lds_bytes'], p['deep_lds_entries'], p['recomputed'])"
   done
 }
 step_shard8() {
