@@ -463,6 +463,7 @@ def synthetic_leg(args, world, rank, local, dev, cpu_group):
             "ms_per_step": 1e3 * elapsed / steps,
             "higher_is_better": True,
             "scaling": "strong",
+            "vs_baseline": None,
             "dtype": "f64",
             "data": DATA["synthetic"],
             "config": {"workload": "synthetic 128 x %d sites GTR+W4 (BASELINE config 4), %d draw%s per step, "

@@ -10,8 +10,8 @@ import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 def latest(kind):
-    """The newest round's committed line of this kind (r04_..., else r03_...)."""
-    for r in ("r04", "r03"):
+    """The newest round's committed line of this kind (r05_..., else r04_..., r03_...)."""
+    for r in ("r05", "r04", "r03"):
         if os.path.exists(os.path.join(ROOT, "profiles", "%s_%s" % (r, kind))):
             return "%s_%s" % (r, kind)
     raise FileNotFoundError(kind)
@@ -20,6 +20,25 @@ def latest(kind):
 LINES = [latest(k) for k in ("fluA_bench.json", "HCV_bench.json", "DS1_bench.json", "synthetic_class_bench.json")]
 KEYS = ["metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
         "vs_baseline", "dtype", "data", "config", "roofline", "cpu_baseline"]
+
+
+def check_roofline(rf):
+    """The pattern sweep is priced against the fp64 vector roof with SURVEY.md
+    8d's algorithmic flops (its HBM view beside it); the class sweep against
+    HBM with the algorithmic bytes.  Either way achieved = algorithmic work of
+    one launch / the kernel's average launch, frac = achieved / peak."""
+    assert rf["frac"] == pytest.approx(rf["achieved"] / rf["peak"], rel=1e-12)
+    t = rf["kernel_avg_ms"] * 1e-3
+    if rf["bound"] == "fp64-vector":
+        assert rf["unit"] == "TFLOP/s" and rf["peak"] == 78.6
+        assert rf["achieved"] == pytest.approx(rf["algorithmic_flops_per_launch"] / t / 1e12, rel=1e-9)
+        hbm = rf["hbm"]
+        assert hbm["unit"] == "GB/s" and hbm["peak"] == 8000.0
+        assert hbm["achieved"] == pytest.approx(hbm["algorithmic_bytes_per_launch"] / t / 1e9, rel=1e-9)
+        assert hbm["frac"] == pytest.approx(hbm["achieved"] / hbm["peak"], rel=1e-12)
+    else:
+        assert rf["bound"] == "hbm" and rf["unit"] == "GB/s" and rf["peak"] == 8000.0
+        assert rf["achieved"] == pytest.approx(rf["algorithmic_bytes_per_launch"] / t / 1e9, rel=1e-9)
 
 
 def last_line(name):
@@ -34,12 +53,7 @@ def test_committed_bench_line_keeps_the_contract(name):
         assert k in d, k
     assert d["n_gpus"] == 1 and d["higher_is_better"] is True and d["dtype"] == "f64"
     assert "workload" in d["config"]
-    rf = d["roofline"]
-    assert rf["bound"] == "hbm" and rf["unit"] == "GB/s" and rf["peak"] == 8000.0
-    assert rf["frac"] == pytest.approx(rf["achieved"] / rf["peak"], rel=1e-12)
-    # achieved = algorithmic bytes of one launch / the kernel's average launch
-    assert rf["achieved"] == pytest.approx(rf["algorithmic_bytes_per_launch"] / (rf["kernel_avg_ms"] * 1e-3) / 1e9,
-                                           rel=1e-9)
+    check_roofline(d["roofline"])
     cb = d["cpu_baseline"]
     for k in ("value", "unit", "cores", "kind", "sample"):
         assert k in cb, k
@@ -67,3 +81,37 @@ def test_pmc_traffic_belongs_to_the_committed_lines():
         assert d["roofline"]["traffic"] == pytest.approx(pmc["per_launch_bytes"]["fluA:8192:pattern"], rel=1e-12)
     else:
         assert d["roofline"]["traffic"] is None
+
+
+def test_default_line_carries_the_synthetic_record():
+    """bench.py's default run (the driver's BENCH line) carries BASELINE
+    config 4 -- the 128 x 1M synthetic alignment, one draw per step -- timed
+    in the same process, with its own roofline, CPU baseline and nominal check
+    (VERDICT r04 next-round item 1)."""
+    d = last_line(latest("fluA_bench.json"))
+    if "synthetic" not in d:
+        pytest.skip("the committed fluA line predates the synthetic sub-record")
+    sy = d["synthetic"]
+    for k in KEYS:
+        assert k in sy, k
+    for k in ("allreduce", "nominal_check", "multidev", "program"):
+        assert k in sy, k
+    assert sy["dtype"] == "f64" and sy["unit"] == "evals/s" and sy["scaling"] == "strong"
+    assert sy["config"]["draws_per_step"] == 1 and sy["config"]["taxa"] == 128
+    assert sy["value"] == pytest.approx(1.0 / (sy["ms_per_step"] * 1e-3), rel=1e-9)
+    check_roofline(sy["roofline"])
+    assert sy["nominal_check"]["ok"] is True
+    assert sy["nominal_check"]["rel_err"] <= 1e-10 and sy["nominal_check"]["grad_blens_max_rel_err"] <= 1e-8
+    cb = sy["cpu_baseline"]
+    assert cb["kind"] == "port" and cb["cores"] == 1 and cb["unit"] == "evals/s"
+    if sy["n_gpus"] == 1:
+        assert sy["multidev"] is None
+
+
+def test_default_line_reports_the_one_draw_sampler_call():
+    d = last_line(latest("fluA_bench.json"))
+    sl = d["sampler_latency"]
+    if "pattern_us_per_call_1draw" not in sl:
+        pytest.skip("the committed fluA line predates the 1-draw figure")
+    assert 0 < sl["pattern_us_per_call_1draw"] < 1e4
+    assert d["draws_100"] is not None
