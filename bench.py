@@ -360,7 +360,7 @@ def synthetic_leg(args, world, rank, local, dev, cpu_group):
     if info["engine"] == "class":
         info.update({"class_" + k: v for k, v in eng.class_info().items()})
     B = eng.B
-    rng = np.random.default_rng(4321 + rank)
+    rng = np.random.default_rng(4321)  # every rank evaluates the same points (its own patterns)
     steps = args.synthetic_steps or max(20, args.steps)
     warm = max(3, min(args.warmup, 10))
     nuniq = min(steps + warm, 8)
@@ -368,11 +368,12 @@ def synthetic_leg(args, world, rank, local, dev, cpu_group):
     d_blens = torch.tensor(blens, device=dev, dtype=torch.float64)
     d_model = torch.tensor(mvs, device=dev, dtype=torch.float64)
     d_out = torch.zeros((draws, eng.outlen), device=dev, dtype=torch.float64)
-    stream = torch.cuda.current_stream(dev).cuda_stream
+    stream = torch.cuda.Stream(device=dev)  # not the null stream: the engine and the collective share it
     setup_s = time.perf_counter() - t_setup
 
     def step(k):
-        sl.evaluate(d_blens[k % nuniq], d_model[k % nuniq], d_out, stream=stream)
+        with torch.cuda.stream(stream):
+            sl.evaluate(d_blens[k % nuniq], d_model[k % nuniq], d_out)
 
     def max_over_ranks(x):
         if world == 1:
@@ -401,16 +402,17 @@ def synthetic_leg(args, world, rank, local, dev, cpu_group):
     eng.timing_start()
     for k in range(steps):
         sl.engine.evaluate_device(d_blens[k % nuniq].data_ptr(), d_model[k % nuniq].data_ptr(), d_out.data_ptr(),
-                                  0, n_draws=draws, stream=stream)
+                                  0, n_draws=draws, stream=stream.cuda_stream)
     torch.cuda.synchronize(dev)
     kern_ms, nl = eng.timing_read()
     kern_avg_ms = max_over_ranks(kern_ms / max(nl, 1))
     allreduce = None
     if world > 1:  # the step's one collective alone: the full fp64 rows, ~130 KB per draw
         buf = torch.zeros_like(d_out)
-        for _ in range(5):
-            dist.all_reduce(buf)
-        ar = timed(lambda k: dist.all_reduce(buf), 50)
+        with torch.cuda.stream(stream):
+            for _ in range(5):
+                dist.all_reduce(buf)
+            ar = timed(lambda k: dist.all_reduce(buf), 50)
         allreduce = dict(us_per_call=1e6 * ar / 50, bytes=buf.numel() * 8, op="all_reduce(SUM) fp64, RCCL")
     step(0)  # parameter set 0, draw 0: the nominal point
     torch.cuda.synchronize(dev)
@@ -567,8 +569,10 @@ def main():
                               else "device-side shard sum (one device)" if n > 1 else "none (one shard)")
 
         def evaluate(self, d_blens, d_model, d_out, stream=None):
+            if stream is None:  # torch's current stream (bench.py's steps run under a non-null one)
+                stream = torch.cuda.current_stream(d_out.device).cuda_stream
             self.engine.evaluate_device(d_blens.data_ptr(), d_model.data_ptr(), d_out.data_ptr(), 0,
-                                        n_draws=d_blens.shape[0], stream=stream or 0)
+                                        n_draws=d_blens.shape[0], stream=stream)
 
     batched = args.workload in BATCHED
     if batched:
@@ -613,18 +617,20 @@ def main():
     B = eng.B
     P_local = sl.p1 - sl.p0
 
-    # pre-generated, distinct parameter points for every step (seeded per rank)
-    rng = np.random.default_rng(1234 + rank)
+    # pre-generated, distinct parameter points for every step (seeded per rank for replicas; the
+    # pattern shards of one evaluation share their points)
+    rng = np.random.default_rng(1234 + (rank if batched else 0))
     nsets = args.warmup + args.steps
     nuniq = min(nsets, 16)
     blens, mvs = parameter_sets(prob, nuniq, draws, B, C, rng)
     d_blens = torch.tensor(blens, device=dev, dtype=torch.float64)
     d_model = torch.tensor(mvs, device=dev, dtype=torch.float64)
     d_out = torch.zeros((draws, eng.outlen), device=dev, dtype=torch.float64)
-    stream = torch.cuda.current_stream(dev).cuda_stream
+    stream = torch.cuda.Stream(device=dev)  # not the null stream: the engine and the collective share it
 
     def step(k):
-        sl.evaluate(d_blens[k % nuniq], d_model[k % nuniq], d_out, stream=stream)
+        with torch.cuda.stream(stream):
+            sl.evaluate(d_blens[k % nuniq], d_model[k % nuniq], d_out)
 
     for k in range(args.warmup):
         step(k)
@@ -672,15 +678,17 @@ def main():
     d_out_c = torch.zeros((draws, eng.outlen), device=dev, dtype=torch.float64)
     h_out = torch.empty((draws, eng.outlen), dtype=torch.float64, pin_memory=True)
     nh = max(1, min(args.steps, 20))
-    for k in range(2):
-        sl.evaluate(d_blens[k % nuniq], d_model[k % nuniq], d_out_c, stream=stream)
+    with torch.cuda.stream(stream):
+        for k in range(2):
+            sl.evaluate(d_blens[k % nuniq], d_model[k % nuniq], d_out_c)
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
     ta = time.perf_counter()
-    for k in range(nh):
-        sl.evaluate(d_blens[k % nuniq], d_model[k % nuniq], d_out_c, stream=stream)
-        h_out.copy_(d_out_c, non_blocking=True)
+    with torch.cuda.stream(stream):
+        for k in range(nh):
+            sl.evaluate(d_blens[k % nuniq], d_model[k % nuniq], d_out_c)
+            h_out.copy_(d_out_c, non_blocking=True)
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
@@ -707,13 +715,13 @@ def main():
         d_out1 = torch.zeros((1, eng.outlen), device=dev, dtype=torch.float64)
         for k in range(10):
             eng.evaluate_device(d_blens[0, :1].data_ptr(), d_model[0, :1].data_ptr(), d_out1.data_ptr(), 0,
-                                n_draws=1, stream=stream)
+                                n_draws=1, stream=stream.cuda_stream)
         torch.cuda.synchronize(dev)
         n1 = 200
         ta = time.perf_counter()
         for k in range(n1):
             eng.evaluate_device(d_blens[k % nuniq, :1].data_ptr(), d_model[k % nuniq, :1].data_ptr(),
-                                d_out1.data_ptr(), 0, n_draws=1, stream=stream)
+                                d_out1.data_ptr(), 0, n_draws=1, stream=stream.cuda_stream)
         torch.cuda.synchronize(dev)
         tb = time.perf_counter()
         single = dict(evals_per_s=n1 / (tb - ta), us_per_eval=1e6 * (tb - ta) / n1)

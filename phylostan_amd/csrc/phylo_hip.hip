@@ -1951,16 +1951,19 @@ constexpr int QFIN_SLOTS = 16;                // workgroup slots per draw it tak
 // atomic loads).  On gfx950 that is the sc1 form of cdna_hip_programming.md
 // Guideline 16 / MI355X_MICROARCH.md "Valid forms" row 1: sc1 stores leave
 // the producer's L2 at once, sc1 loads bypass the reader's L1, and the add is
-// issued after the drain -- the reader cannot see a stale copy.  It is
-// ISA-level, not a C++-model, guarantee (relaxed atomics on both sides).  The
-// model-level form adds ONE agent-scope acquire in the last workgroup after
-// its ticket (the guide's R1 consume recipe; the producers' sc1 payload needs
-// no release fence): PHY_HANDOFF_ACQUIRE=1 at build time selects it, measured
-// in DESIGN.md (it sits on the call's critical path); the default keeps the
-// sc1 form, guarded by tests/test_gpu_quad.py / test_gpu_class.py stress tests
-// (10^4 calls, rows compared bitwise, one process).
+// issued after the drain -- the reader cannot see a stale copy.  On top of
+// that the last workgroup takes ONE agent-scope acquire after its ticket (the
+// guide's Consumer recipe: relaxed ticket -> agent acquire -> vmcnt wait ->
+// barrier), so the hand-off does not rest on the sc1-load argument alone; the
+// producers' sc1 payload + drain needs no release fence (MI355X_MICROARCH
+// "Valid forms", Consumer (2)-(3)).  Measured on one box, alternating: fluA
+// 4-draw call 103.8 / 103.8 us without / with, 1-draw 99.1 / 100.6, shard of 8
+// 3,984 / 3,986 evals/s (profiles/r05_handoff_acquire_ab.txt) -- within noise,
+// so it is the default; PHY_HANDOFF_ACQUIRE=0 at build time gives the
+// sc1-only form.  tests/test_gpu_quad.py / test_gpu_class.py stress tests run
+// 10^4 calls with rows compared bitwise, in one process.
 #ifndef PHY_HANDOFF_ACQUIRE
-#define PHY_HANDOFF_ACQUIRE 0
+#define PHY_HANDOFF_ACQUIRE 1
 #endif
 __device__ __forceinline__ void handoff_acquire(bool last) {
   if (PHY_HANDOFF_ACQUIRE && last) {

@@ -69,19 +69,31 @@ class ShardedLikelihood:
     def evaluate(self, blens, model, out, site_ll=None, stream=None, group=None):
         """blens [n, B], model [n, 10+2C], out [n, outlen]: device tensors.
 
-        The sweep runs on ``stream`` (default: torch's current stream of
-        ``out``'s device), the stream RCCL's ``all_reduce`` orders itself
-        against, so the reduction reads ``out`` only after the kernels wrote
-        it and the kernels read blens / model only after torch produced them.
+        The sweep is ordered on torch's current stream of ``out``'s device
+        (or on ``stream``, a hipStream_t handle), the stream the collective
+        orders itself against, so the reduction reads ``out`` only after the
+        kernels wrote it and the kernels read blens / model only after torch
+        produced them.  torch's default stream is the null stream (handle 0),
+        which the C boundary reads as "the context's own stream"
+        (include/phylo_hip.h phy_eval_device): on it the sweep runs on a side
+        stream fenced both ways with events instead.
         """
         import torch
         import torch.distributed as dist
         n = blens.shape[0]
-        if stream is None:
-            stream = torch.cuda.current_stream(out.device).cuda_stream if out.is_cuda else 0
-        self.engine.evaluate_device(blens.data_ptr(), model.data_ptr(), out.data_ptr(),
-                                    site_ll.data_ptr() if site_ll is not None else 0, n_draws=n,
-                                    stream=stream)
+        args = (blens.data_ptr(), model.data_ptr(), out.data_ptr(),
+                site_ll.data_ptr() if site_ll is not None else 0)
+        if stream is None and out.is_cuda:
+            stream = torch.cuda.current_stream(out.device).cuda_stream
+        if out.is_cuda and not stream:
+            cur = torch.cuda.current_stream(out.device)
+            if getattr(self, "_side", None) is None:
+                self._side = torch.cuda.Stream(device=out.device)
+            self._side.wait_stream(cur)
+            self.engine.evaluate_device(*args, n_draws=n, stream=self._side.cuda_stream)
+            cur.wait_stream(self._side)
+        else:
+            self.engine.evaluate_device(*args, n_draws=n, stream=stream)
         if self.world > 1:
             dist.all_reduce(out, op=dist.ReduceOp.SUM, group=group)
         return out

@@ -22,6 +22,11 @@ pytestmark = pytest.mark.gpu
 def _case(name):
     if name == "HCV":
         return cases.hcv_case()
+    if name == "syn200k":  # the class sweep: long enough that a reduction racing the kernels would show
+        from phylostan_amd import synthetic
+        pd, prm = synthetic.simulate(n_sites=200_000)
+        return cases.Case("syn200k", pd.tipcodes, pd.weights, pd.peel0, True, "GTR", 4, prm["blens"], prm["freqs"],
+                          prm["rates"], prm["rs"], prm["ps"])
     return cases.random_case(11, S=40, P=700, C=3, model="GTR", rooted=True)
 
 
@@ -40,7 +45,9 @@ def _worker(rank, world, port, name, q):
         blens = torch.tensor(np.stack([case.blens, case.blens * 1.2]), device=dev)
         model = torch.tensor(np.stack([case.model_vec(), case.model_vec()]), device=dev)
         out = torch.full((2, sl.outlen), float("nan"), dtype=torch.float64, device=dev)
-        sl.evaluate(blens, model, out)
+        for _ in range(3):  # back-to-back steps on torch's default (null) stream, as a training loop issues them
+            out.fill_(float("nan"))
+            sl.evaluate(blens, model, out)
         res = out.cpu().numpy()
         if rank == 0:
             q.put((sl.p0, sl.p1, res))
@@ -55,7 +62,7 @@ def _free_port():
         return s.getsockname()[1]
 
 
-@pytest.mark.parametrize("name,world", [("HCV", 2), ("random", 3)])
+@pytest.mark.parametrize("name,world", [("HCV", 2), ("random", 3), ("syn200k", 2)])
 def test_sharded_device_allreduce_equals_whole(name, world):
     from phylostan_amd.engine import TreeLikelihood
     ctx = mp.get_context("spawn")
