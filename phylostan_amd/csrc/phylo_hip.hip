@@ -2824,6 +2824,7 @@ int launch_class(phy_ctx* ctx, int n, const double* d_blens, const double* d_mod
     if (L.ntile) {
       a.first = L.tile0;
       a.count = L.ntile;
+      a.sfirst = L.sec0;
       hipLaunchKernelGGL(cls_red_kernel, dim3((L.ntile + CLS_WPG - 1) / CLS_WPG, dcn), dim3(CLS_THREADS), 0, st, a);
     }
     if (L.nlfix)  // the level's long spans (the short ones are summed by the REV lanes)

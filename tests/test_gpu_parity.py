@@ -486,13 +486,14 @@ def test_retired_resident_engine_is_refused():
     assert eng.engine() == "pattern"
 
 
-def test_block_wave_plan_rows_bitwise_equal(monkeypatch):
+def test_block_wave_plan_rows_equal(monkeypatch):
     """The opt-in block-wave plan (PHY_WB=1: a workgroup of C x 2 waves runs
     two pattern blocks over one LDS chunk holding every matrix record) forms
-    the same sums in the same order as the default plan -- the second
-    block's dL/dP added to the first's (slot sum instead of atomic add), the
-    rebuilt cherries the same arithmetic as stored ones -- so every output
-    row of a 256-draw fluA launch is bitwise the default plan's."""
+    the same terms as the default plan; its per-draw partial sums (dL/dP,
+    scalars) meet in another order (block-wave slots summed by the epilogue
+    instead of one wave's running sum), so every output row of a 256-draw
+    fluA launch agrees with the default plan's to a few ulps, not bit for
+    bit."""
     from phylostan_amd import models
     from phylostan_amd.engine import TreeLikelihood
     base = cases.fluA_case()
@@ -508,4 +509,6 @@ def test_block_wave_plan_rows_bitwise_equal(monkeypatch):
         plan = eng.lds_plan()
         assert plan["n_chunks"] == (1 if wb == "1" else 2), plan
         rows[wb] = eng.evaluate_rows(blens, mvs)
-    assert np.array_equal(rows["0"], rows["1"])
+    a, b = rows["0"], rows["1"]
+    scale = np.maximum(np.abs(a).max(axis=0), 1e-300)
+    assert np.max(np.abs(a - b) / scale) < 1e-12

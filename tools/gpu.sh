@@ -33,6 +33,11 @@ step_flow() {  # the dataflow class launch: bitwise against the level launches, 
     > $O/pytest_flow.log 2>&1 || { tail -40 $O/pytest_flow.log; exit 1; }
   tail -12 $O/pytest_flow.log
 }
+step_stress() {  # the relaxed hand-off stress tests: 10^4 calls each, outputs bitwise (quad epilogue, class flow)
+  timeout -k 10 600 python -u -m pytest tests/test_gpu_quad.py tests/test_gpu_class.py -x -v -k stress --timeout 400 \
+    --timeout-method thread > $O/pytest_stress.log 2>&1 || { tail -30 $O/pytest_stress.log; exit 1; }
+  tail -6 $O/pytest_stress.log
+}
 step_smoke() {
   timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1
   tail -3 $O/smoke.log
@@ -115,7 +120,7 @@ step_latab() {  # sampler-call latency A/B: LAT_WLS x LAT_DRAWS over AB_VARIANTS
       done
     done
   done
-  [ -n "${LAT_TRACE:-1}" ] || return 0
+  [ -n "${LAT_TRACE-1}" ] || return 0
   local d=${LAT_TRACE_DRAWS:-100}
   for v in $V; do  # that call's kernels on the device clock
     n=$(vname $v)
@@ -154,6 +159,7 @@ step_shard8() {
   timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof_shard8 -o run -- \
     python bench.py --workload synthetic --shard-of 8 --steps 50 --warmup 5 --no-cpu-baseline \
     > $O/prof_shard8.log 2>&1
+  python tools/eval_timeline.py $O/prof_shard8/run_results.db > $O/timeline_shard8.txt && tail -22 $O/timeline_shard8.txt
 }
 step_synth() {
   timeout -k 10 300 python bench.py --workload synthetic --steps 50 --warmup 5 --no-cpu-baseline \
@@ -161,6 +167,7 @@ step_synth() {
   python -c "import json;d=json.load(open('$O/bench_synth.json'));print('synth', d['value'], d['ms_per_step'])"
   timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof_synth -o run -- \
     python bench.py --workload synthetic --steps 30 --warmup 5 --no-cpu-baseline > $O/prof_synth.log 2>&1
+  python tools/eval_timeline.py $O/prof_synth/run_results.db > $O/timeline_synth.txt && tail -22 $O/timeline_synth.txt
 }
 step_multidev() {
   timeout -k 10 300 python bench.py --workload synthetic --multi-device 1 --steps 30 --warmup 5 \
