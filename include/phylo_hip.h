@@ -268,6 +268,17 @@ int phy_class_info(const phy_ctx* ctx, long long* classes, int* levels, int* roo
  * Results are bitwise the same either way. */
 int phy_class_clades(const phy_ctx* ctx, int* fused_levels, int* clades, long long* largest);
 
+/* Top chain of the class plan: the run of single-node levels below the root
+ * (caterpillar-like trees), fused into one forward and one reverse launch
+ * (one lane per class of the top node, the classes below it from host
+ * tables); chain levels (0: none), the lowest chained level and the top
+ * node's classes.  Chosen when at least two such levels lie above the clade
+ * levels (at most 8); PHY_CHAIN=0 at phy_create turns it off.  The forward
+ * values are bitwise the level launches'; the dL/dP sums of the chained
+ * branches run over the top classes, so they agree to rounding, not bits.
+ * A plan with a chain has no dataflow launch (phy_set_flow has no effect). */
+int phy_class_chain(const phy_ctx* ctx, int* levels, int* lowest, int* top_classes);
+
 #ifdef __cplusplus
 }
 #endif

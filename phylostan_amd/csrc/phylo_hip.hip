@@ -2732,8 +2732,10 @@ int select_engine(phy_ctx* c) {
 
 // The class sweep runs as the dataflow launch (cls_flow_kernel) when it is
 // preferred and allowed and the categories fit its workgroup (C waves <= 16).
+// (a plan with a top chain has no dataflow items: build with PHY_CHAIN=0 for it)
 bool flow_applies(const phy_ctx* ctx) {
-  return ctx->flow_pref && ctx->flow_ok && ctx->C <= 16 && ctx->flow_wgs[0] > 0 && ctx->flow_wgs[1] > 0;
+  return ctx->flow_pref && ctx->flow_ok && ctx->C <= 16 && ctx->flow_wgs[0] > 0 && ctx->flow_wgs[1] > 0 &&
+         !(ctx->ce && ctx->ce->chain_m > 0);
 }
 
 // HIP events around the timed part of one launch (phy_timing_start)
@@ -2807,13 +2809,21 @@ int launch_class(phy_ctx* ctx, int n, const double* d_blens, const double* d_mod
   if (!flow && e->Lc > 0)  // levels 1..Lc: one workgroup per (bottom clade, dc)
     hipLaunchKernelGGL(cls_clade_fwd_kernel, dim3(e->nclade, dcn), dim3(CLADE_THREADS), 0, st, a,
                        (const CladeLevel*)e->d_clade, e->Lc);
+  const bool chain = !flow && e->chain_m > 0;
+  const ChainArgs ca{e->d_link, e->d_ctab, e->d_crep, e->chain_m, e->chain_ntop, e->chain_ntp, e->chain_toff};
+  const int chain_wgs = (e->chain_ntp / WAVE + CLS_WPG - 1) / CLS_WPG;
+  auto in_chain = [&](int l) { return chain && l >= e->chain_lo && l <= e->chain_hi; };
   for (int l = e->Lc + 1; l < e->levels && !flow; ++l) {
     const ClassLevel& L = e->lv[l];
-    if (!L.nchunk) continue;
+    if (!L.nchunk || in_chain(l)) continue;
     a.first = L.chunk0;
     a.count = L.nchunk;
     hipLaunchKernelGGL(cls_fwd_kernel, dim3((L.nchunk + CLS_WPG - 1) / CLS_WPG, dcn), dim3(CLS_THREADS), 0, st, a);
   }
+  if (chain)  // levels lo..hi in one launch
+    hipLaunchKernelGGL(e->chain_m <= 4 ? cls_chain_fwd_kernel<4>
+                       : e->chain_m <= 6 ? cls_chain_fwd_kernel<6> : cls_chain_fwd_kernel<CHAIN_MAX>,
+                       dim3(chain_wgs, dcn), dim3(CLS_THREADS), 0, st, a, ca);
   if (!flow) {
     auto rk = C <= 4 ? (e->root_tips ? cls_root_kernel<256, true> : cls_root_kernel<256, false>)
                      : (e->root_tips ? cls_root_kernel<1024, true> : cls_root_kernel<1024, false>);
@@ -2830,6 +2840,13 @@ int launch_class(phy_ctx* ctx, int n, const double* d_blens, const double* d_mod
     if (L.nlfix)  // the level's long spans (the short ones are summed by the REV lanes)
       hipLaunchKernelGGL(cls_fix_list_kernel, dim3((L.nlfix + CLS_WPG - 1) / CLS_WPG, dcn), dim3(CLS_THREADS), 0, st, a,
                          (const int*)e->d_lfix + L.lfix0, L.nlfix);
+    if (in_chain(l)) {  // the chain's levels: one reverse launch at its top (levels below hold no staged tiles)
+      if (l == e->chain_hi)
+        hipLaunchKernelGGL(e->chain_m <= 4 ? cls_chain_rev_kernel<4>
+                           : e->chain_m <= 6 ? cls_chain_rev_kernel<6> : cls_chain_rev_kernel<CHAIN_MAX>,
+                           dim3(chain_wgs, dcn), dim3(CLS_THREADS), 0, st, a, ca);
+      continue;
+    }
     if (L.nchunk) {
       a.first = L.chunk0;
       a.count = L.nchunk;
@@ -3895,6 +3912,16 @@ int phy_class_info(const phy_ctx* ctx, long long* classes, int* levels, int* roo
   if (staged) *staged = e ? e->stage_sec : 0;
   if (tiles) *tiles = e ? e->ntiles : 0;
   if (spans) *spans = nspan;
+  return PHY_OK;
+}
+
+int phy_class_chain(const phy_ctx* ctx, int* levels, int* lowest, int* top_classes) {
+  if (!ctx) return fail(PHY_EINVAL, "NULL ctx");
+  if (ctx->ms) return phy_class_chain(ctx->ms->shard[0], levels, lowest, top_classes);
+  const ClassEngine* e = ctx->ce;
+  if (levels) *levels = e ? e->chain_m : 0;
+  if (lowest) *lowest = e && e->chain_m ? e->chain_lo : 0;
+  if (top_classes) *top_classes = e ? e->chain_ntop : 0;
   return PHY_OK;
 }
 

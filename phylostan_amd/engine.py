@@ -341,9 +341,13 @@ class TreeLikelihood:
         fl, nc, big = ctypes.c_int(), ctypes.c_int(), ctypes.c_longlong()
         _lib.check(self.lib.phy_class_clades(self.ctx, ctypes.byref(fl), ctypes.byref(nc), ctypes.byref(big)),
                    "phy_class_clades")
+        cl, clo, ctop = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
+        _lib.check(self.lib.phy_class_chain(self.ctx, ctypes.byref(cl), ctypes.byref(clo), ctypes.byref(ctop)),
+                   "phy_class_chain")
         return dict(classes=ll[0].value, levels=ii[0].value, root_classes=ii[1].value, stage=ll[1].value,
                     staged=ll[2].value, tiles=ii[2].value, spans=ii[3].value, clade_levels=fl.value,
-                    clades=nc.value, clade_max=big.value)
+                    clades=nc.value, clade_max=big.value, chain_levels=cl.value, chain_lowest=clo.value,
+                    chain_top_classes=ctop.value)
 
     def timing_start(self):
         _lib.check(self.lib.phy_timing_start(self.ctx), "phy_timing_start")

@@ -5,6 +5,8 @@ against the CPU oracle, through the C-ABI with phy_set_engine(2).
 Same bar as tests/test_gpu_parity.py: per-site and total log L rel 1e-10,
 every gradient rel 1e-9 of its array's largest entry.
 """
+import os
+
 import numpy as np
 import pytest
 
@@ -105,19 +107,22 @@ def test_class_sweep_deterministic_and_agrees_with_pattern_sweep():
 
 
 def _with_clade(case, value, max_draws=1):
-    import os
-    old = os.environ.get("PHY_CLADE")
+    # (chain-free plans: the top chain starts above the clade levels, so its
+    # extent -- and the order of its dL/dP sums -- would follow the clade depth)
+    old = os.environ.get("PHY_CLADE"), os.environ.get("PHY_CHAIN")
     if value is None:
         os.environ.pop("PHY_CLADE", None)
     else:
         os.environ["PHY_CLADE"] = str(value)
+    os.environ["PHY_CHAIN"] = "0"
     try:
         return _class_engine(case, max_draws=max_draws)
     finally:
-        if old is None:
-            os.environ.pop("PHY_CLADE", None)
-        else:
-            os.environ["PHY_CLADE"] = old
+        for k, v in zip(("PHY_CLADE", "PHY_CHAIN"), old):
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
 
 
 @pytest.mark.parametrize("seed,S,P,C,model,rooted,cat", [
@@ -165,13 +170,23 @@ def test_class_clades_repetitive_alignment_bitwise():
 
 
 def _flow_pair(case, max_draws=1):
-    eng = _class_engine(case, max_draws=max_draws)
-    assert not eng.flow()  # opt-in
-    eng.set_flow(True)
-    assert eng.flow()
-    lvl = _class_engine(case, max_draws=max_draws)
-    lvl.set_flow(False)
-    assert not lvl.flow()
+    # the dataflow launch has no items for the top chain: both plans chain-free
+    old = os.environ.get("PHY_CHAIN")
+    os.environ["PHY_CHAIN"] = "0"
+    try:
+        eng = _class_engine(case, max_draws=max_draws)
+        assert not eng.flow()  # opt-in
+        eng.set_flow(True)
+        assert eng.flow()
+        lvl = _class_engine(case, max_draws=max_draws)
+        lvl.set_flow(False)
+        assert not lvl.flow()
+    finally:
+        if old is None:
+            del os.environ["PHY_CHAIN"]
+        else:
+            os.environ["PHY_CHAIN"] = old
+    assert eng.class_info()["chain_levels"] == 0
     return eng, lvl
 
 
@@ -252,3 +267,61 @@ def test_class_flow_stress_bitwise_over_many_calls():
             bad += (out != first).any().to(torch.int64)
         stream.synchronize()
     assert int(bad.item()) == 0
+
+
+def _chain_pair(case, monkeypatch, max_draws=1):
+    """The same plan with and without the top chain (PHY_CHAIN=0)."""
+    monkeypatch.setenv("PHY_CHAIN", "0")
+    plain = _class_engine(case, max_draws=max_draws)
+    monkeypatch.delenv("PHY_CHAIN")
+    chained = _class_engine(case, max_draws=max_draws)
+    assert plain.class_info()["chain_levels"] == 0
+    return chained, plain
+
+
+@pytest.mark.parametrize("make", [cases.fluA_case, cases.hcv_case, cases.ds1_case, "syn200k", "caterpillar"],
+                         ids=["fluA", "HCV", "DS1_unrooted", "synthetic200k", "caterpillar_random"])
+def test_class_chain_equals_level_launches(make, monkeypatch):
+    """The top chain (the single-node levels below the root in one forward and
+    one reverse launch, one lane per top class) forms the level launches'
+    forward values bit for bit -- site log-likelihoods and log-likelihood
+    identical -- and the same gradients up to the order of the dL/dP sums of
+    the chained branches (over top classes instead of each node's classes);
+    both at the parity bar against the oracle."""
+    if make == "syn200k":
+        from phylostan_amd import synthetic
+        pd, prm = synthetic.simulate(n_sites=200_000)
+        case = cases.Case("syn200k", pd.tipcodes, pd.weights, pd.peel0, True, "GTR", 4, prm["blens"], prm["freqs"],
+                          prm["rates"], prm["rs"], prm["ps"])
+    elif make == "caterpillar":
+        case = cases.random_case(5, S=40, P=2000, C=3, model="GTR", rooted=True, caterpillar=True)
+    else:
+        case = make()
+    chained, plain = _chain_pair(case, monkeypatch)
+    info = chained.class_info()
+    assert info["chain_levels"] >= 2, info
+    a = chained.evaluate(case.blens, case.model_vec(), site_ll=True)
+    b = plain.evaluate(case.blens, case.model_vec(), site_ll=True)
+    assert a.loglik == b.loglik
+    assert np.array_equal(a.site_ll, b.site_ll)
+    for k in ("dLdP", "grad_blens", "grad_rs", "grad_ps", "grad_freq_root", "grad_rates", "grad_freqs"):
+        x, y = np.asarray(getattr(a, k)), np.asarray(getattr(b, k))
+        scale = max(float(np.max(np.abs(y))), 1e-300)
+        assert float(np.max(np.abs(x - y))) <= 1e-12 * scale, k
+    check_case(case, chained, a)
+
+
+def test_class_chain_batched_draws_and_repeats(monkeypatch):
+    """Chained plan, 16 draws per launch: every row equals its single-draw
+    evaluation bit for bit, and repeated launches are bitwise reproducible."""
+    case = cases.hcv_case()
+    eng = _class_engine(case, max_draws=16)
+    assert eng.class_info()["chain_levels"] >= 2
+    rng = np.random.default_rng(3)
+    bl = case.blens[None, :] * rng.uniform(0.7, 1.3, (16, case.blens.size))
+    mv = np.repeat(case.model_vec()[None], 16, axis=0)
+    rows = eng.evaluate_rows(bl, mv)
+    assert np.array_equal(rows, eng.evaluate_rows(bl, mv))
+    one = _class_engine(case, max_draws=1)
+    for k in (0, 7, 15):
+        assert np.array_equal(one.evaluate_rows(bl[k:k + 1], mv[k:k + 1])[0], rows[k])
