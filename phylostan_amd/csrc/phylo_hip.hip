@@ -2209,6 +2209,12 @@ struct phy_ctx {
   bool eig_fuse_pref = true;   // PHY_EIG_FUSE=0: small device batches take eig_kernel + pmat_kernel<false>
   // the quad sweep (quad_engine.inc) for calls of <= QUAD_MAX_DRAWS draws
   bool quad_pref = true;       // PHY_QUAD=0: off
+  // the multi-wave quad sweep (qmw_kernel): W waves per category share a block
+  bool qmw_pref = true;        // PHY_QMW=0: the one-wave quad sweep
+  bool qmw_ok = false;
+  int qmw_W = 0, qmw_maxst = 0, qmw_nslot = 0, qmw_root = 0, qmw_nst[4] = {0, 0, 0, 0};
+  size_t qmw_lds = 0;
+  int* d_mprog = nullptr;
   bool quad_ok = false;        // its LDS plan fits
   size_t quad_lds = 0;
   int* d_qprog = nullptr;      // unpacked program, nothing rebuilt (every moved partial stored)
@@ -2305,7 +2311,7 @@ void free_ctx(phy_ctx* c) {
   void* ptrs[] = {c->d_tips,  c->d_w,     c->d_prog,    c->d_gpos,    c->d_mat_branch, c->d_pmat,
                   c->d_eig,   c->d_inner, c->d_model,   c->d_blens,   c->d_out,        c->d_site,
                   c->d_scratch, c->d_dstk, c->d_gslot,  c->d_sslot, c->d_grows, c->d_in, c->d_qprog, c->d_qscr,
-                  c->d_qfpart, c->d_qfcnt};
+                  c->d_qfpart, c->d_qfcnt, c->d_mprog};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   if (c->h_in) (void)hipHostFree(c->h_in);
@@ -3069,10 +3075,18 @@ int launch_quad(phy_ctx* ctx, int n, const double* d_blens, const double* d_mode
     if (rc) return rc;
   }
   {
-    const int* prog = ctx->d_qprog;
-    void* kargs[] = {(void*)&qa, (void*)&prog};
-    const void* kern = C <= 4 ? (const void*)qsweep_kernel<256> : (const void*)qsweep_kernel<1024>;
-    HIP_TRY(hipLaunchKernel(kern, dim3(gx, n), dim3(C * WAVE), kargs, ctx->quad_lds, st));
+    if (ctx->qmw_ok && ctx->qmw_pref) {  // W waves per category
+      QmwArgs ma{qa, ctx->d_mprog, ctx->qmw_W, ctx->qmw_maxst, ctx->qmw_nslot, ctx->qmw_root,
+                 ctx->qmw_nst[0], ctx->qmw_nst[1], ctx->qmw_nst[2], ctx->qmw_nst[3]};
+      void* kargs[] = {(void*)&ma};
+      HIP_TRY(hipLaunchKernel((const void*)qmw_kernel, dim3(gx, n), dim3(C * ctx->qmw_W * WAVE), kargs, ctx->qmw_lds,
+                              st));
+    } else {
+      const int* prog = ctx->d_qprog;
+      void* kargs[] = {(void*)&qa, (void*)&prog};
+      const void* kern = C <= 4 ? (const void*)qsweep_kernel<256> : (const void*)qsweep_kernel<1024>;
+      HIP_TRY(hipLaunchKernel(kern, dim3(gx, n), dim3(C * WAVE), kargs, ctx->quad_lds, st));
+    }
   }
   HIP_TRY(hipGetLastError());
   if (ctx->timing) HIP_TRY(hipEventRecord(e1, st));
@@ -3300,6 +3314,8 @@ int phy_create(int S, int P, int C, int rooted, int model, const uint8_t* tipcod
     c->eig_fuse_pref = env_flag("PHY_EIG_FUSE", 1);
     const char* qk2 = getenv("PHY_QUAD");
     c->quad_pref = qk2 ? atoi(qk2) != 0 : true;
+    const char* qm = getenv("PHY_QMW");
+    c->qmw_pref = qm ? atoi(qm) != 0 : true;
     c->wb_pref = env_flag("PHY_WB", 0);  // opt-in: measured slower
 
   }
@@ -3342,7 +3358,7 @@ int phy_create(int S, int P, int C, int rooted, int model, const uint8_t* tipcod
     (void)hipFuncSetAttribute(sweep_kernel_ptr(2, true, false, 2), hipFuncAttributeMaxDynamicSharedMemorySize,
                               (int)LDS_CAP);
     (void)hipFuncSetAttribute((const void*)finalize_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)LDS_CAP);
-    for (const void* kern : {(const void*)qsweep_kernel<256>, (const void*)qsweep_kernel<1024>}) {
+    for (const void* kern : {(const void*)qsweep_kernel<256>, (const void*)qsweep_kernel<1024>, (const void*)qmw_kernel}) {
       hipFuncAttributes fa{};  // its static eigensystem copy counts against the cap too
       const size_t stat = hipFuncGetAttributes(&fa, kern) == hipSuccess ? fa.sharedSizeBytes : 1024;
       (void)hipFuncSetAttribute(kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)(LDS_CAP - stat));
@@ -3451,6 +3467,23 @@ int phy_create(int S, int P, int C, int rooted, int model, const uint8_t* tipcod
       const std::vector<int> qp = quad_program(c->prog, c->nsteps, C, c->R);
       TRY_C(dalloc(&c->d_qprog, qp.size()));
       HIP_C(hipMemcpy(c->d_qprog, qp.data(), qp.size() * sizeof(int), hipMemcpyHostToDevice));
+      // the multi-wave variant: as many waves per category as a 1024-thread workgroup holds (<= 4)
+      const int W = std::min(QMW_MAXW, 16 / C);
+      QmwPlan mp;
+      if (W >= 2 && quad_mw_plan(c->prog, qp, c->nsteps, W, mp)) {
+        const size_t lds = qmw_lds_bytes(S, C, c->nmat, c->R, mp.nslot);
+        if (lds + EIG_LEN * sizeof(double) <= LDS_CAP) {
+          TRY_C(dalloc(&c->d_mprog, mp.prog.size()));
+          HIP_C(hipMemcpy(c->d_mprog, mp.prog.data(), mp.prog.size() * sizeof(int), hipMemcpyHostToDevice));
+          c->qmw_ok = true;
+          c->qmw_W = mp.W;
+          c->qmw_maxst = mp.maxst;
+          c->qmw_nslot = mp.nslot;
+          c->qmw_root = mp.root_wave;
+          for (int k = 0; k < 4; ++k) c->qmw_nst[k] = mp.nst[k];
+          c->qmw_lds = lds;
+        }
+      }
     }
   }
   c->h_tips.assign(tipcodes, tipcodes + (size_t)S * P);

@@ -162,3 +162,49 @@ def test_quad_epilogue_handoffs_stress_bitwise(name, monkeypatch):
     for _ in range(10000):
         bad += int(not np.array_equal(eng.evaluate_rows(bl, mv), first))
     assert bad == 0
+
+
+@pytest.mark.parametrize("name", ["fluA", "HCV", "DS1", "rand_C1_JC", "rand_C3_GTR", "unrooted_C5", "many_blocks",
+                                  "caterpillar", "balanced"])
+@pytest.mark.parametrize("n", [1, 4, 16])
+def test_quad_multiwave_rows_bitwise_equal_one_wave(name, n, monkeypatch):
+    """The multi-wave quad sweep (qmw_kernel: the post-order program split
+    over up to 4 waves per category by the host list-scheduler, LDS slot
+    hand-offs with flags) runs every step's arithmetic of the one-wave sweep
+    and writes every dL/dP entry from the one wave owning its step: the rows,
+    site log-likelihoods included, are bitwise PHY_QMW=0's."""
+    make = {"caterpillar": lambda: cases.random_case(305, S=40, P=300, C=4, model="GTR", caterpillar=True),
+            "balanced": lambda: cases.random_case(306, S=64, P=400, C=4, model="HKY")}.get(name, CASES.get(name))
+    case = make()
+    bl, mv = _draws(case, n, 41)
+    out = {}
+    for qmw in ("0", "1"):
+        monkeypatch.setenv("PHY_QMW", qmw)
+        eng = _engine(case, max_draws=n, monkeypatch=monkeypatch)
+        out[qmw] = eng.evaluate_rows(bl, mv)
+        if n == 1:
+            out[qmw + "s"] = eng.evaluate(case.blens, case.model_vec(), site_ll=True).site_ll
+    assert np.array_equal(out["0"], out["1"])
+    if n == 1:
+        assert np.array_equal(out["0s"], out["1s"])
+
+
+def test_quad_multiwave_stress_bitwise(monkeypatch):
+    """2,000 back-to-back 4-draw fluA calls on the multi-wave sweep: every row
+    bitwise the first call's (the slot hand-offs never read a stale value)."""
+    import torch
+    from phylostan_amd.engine import TreeLikelihood
+    monkeypatch.setenv("PHY_QMW", "1")
+    case = cases.fluA_case()
+    eng = TreeLikelihood(case.tipcodes, case.weights, case.peel0, case.rooted, case.model, case.C, max_draws=4)
+    bl, mv = _draws(case, 4, 43)
+    ref = eng.evaluate_rows(bl, mv)
+    d_bl = torch.tensor(bl, device="cuda:0")
+    d_mv = torch.tensor(mv, device="cuda:0")
+    d_out = torch.zeros((2000, 4, eng.outlen), dtype=torch.float64, device="cuda:0")
+    s = torch.cuda.Stream()
+    for k in range(2000):
+        eng.evaluate_device(d_bl.data_ptr(), d_mv.data_ptr(), d_out[k].data_ptr(), 0, n_draws=4, stream=s.cuda_stream)
+    torch.cuda.synchronize()
+    got = d_out.cpu().numpy()
+    assert np.array_equal(got, np.broadcast_to(ref, got.shape))
