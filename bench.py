@@ -413,7 +413,7 @@ def synthetic_leg(args, world, rank, local, dev, cpu_group):
             for _ in range(5):
                 dist.all_reduce(buf)
             ar = timed(lambda k: dist.all_reduce(buf), 50)
-        allreduce = dict(us_per_call=1e6 * ar / 50, bytes=buf.numel() * 8, op="all_reduce(SUM) fp64, RCCL")
+        allreduce = dict(us_per_call=1e6 * ar / 50, bytes=buf.numel() * 8, op="all_reduce(SUM) fp64, %s" % ("RCCL" if dist.get_backend() == "nccl" else dist.get_backend()))
     step(0)  # parameter set 0, draw 0: the nominal point
     torch.cuda.synchronize(dev)
     row0 = d_out[0].double().cpu().numpy()
@@ -752,6 +752,7 @@ def main():
 
         for name in ("pattern",):
             lk = sampler_ctx(name, 4)
+            sampler["quad_plan"] = lk.quad_plan()  # the multi-wave small-call sweep
             for _ in range(20):
                 lk.evaluate_rows(bl4, mv4)
             ta = time.perf_counter()

@@ -279,6 +279,15 @@ int phy_class_clades(const phy_ctx* ctx, int* fused_levels, int* clades, long lo
  * A plan with a chain has no dataflow launch (phy_set_flow has no effect). */
 int phy_class_chain(const phy_ctx* ctx, int* levels, int* lowest, int* top_classes);
 
+/* The sampler's small-call sweep (calls of <= 16 draws, the quad sweep):
+ * waves per category (0: the quad sweep does not apply to this context, 1:
+ * the one-wave quad sweep, 2-4: the multi-wave form, whose host list-schedule
+ * splits the post-order program over that many waves with LDS hand-offs),
+ * the schedule's length in program steps (the one-wave sweep: every step),
+ * and its LDS hand-off slots.  PHY_QMW=0 at phy_create keeps the one-wave
+ * form; the rows are bitwise the same either way. */
+int phy_quad_plan(const phy_ctx* ctx, int* waves, int* span, int* slots);
+
 #ifdef __cplusplus
 }
 #endif

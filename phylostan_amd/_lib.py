@@ -63,6 +63,7 @@ SIGNATURES = {
                                       _c_int_p, _c_int_p]),
     "phy_class_clades": (ctypes.c_int, [ctypes.c_void_p, _c_int_p, _c_int_p, ctypes.POINTER(ctypes.c_longlong)]),
     "phy_class_chain": (ctypes.c_int, [ctypes.c_void_p, _c_int_p, _c_int_p, _c_int_p]),
+    "phy_quad_plan": (ctypes.c_int, [ctypes.c_void_p, _c_int_p, _c_int_p, _c_int_p]),
 }
 
 

@@ -2212,7 +2212,7 @@ struct phy_ctx {
   // the multi-wave quad sweep (qmw_kernel): W waves per category share a block
   bool qmw_pref = true;        // PHY_QMW=0: the one-wave quad sweep
   bool qmw_ok = false;
-  int qmw_W = 0, qmw_maxst = 0, qmw_nslot = 0, qmw_root = 0, qmw_nst[4] = {0, 0, 0, 0};
+  int qmw_W = 0, qmw_maxst = 0, qmw_nslot = 0, qmw_root = 0, qmw_nst[4] = {0, 0, 0, 0}, qmw_span = 0;
   size_t qmw_lds = 0;
   int* d_mprog = nullptr;
   bool quad_ok = false;        // its LDS plan fits
@@ -3480,6 +3480,7 @@ int phy_create(int S, int P, int C, int rooted, int model, const uint8_t* tipcod
           c->qmw_maxst = mp.maxst;
           c->qmw_nslot = mp.nslot;
           c->qmw_root = mp.root_wave;
+          c->qmw_span = mp.span;
           for (int k = 0; k < 4; ++k) c->qmw_nst[k] = mp.nst[k];
           c->qmw_lds = lds;
         }
@@ -3945,6 +3946,16 @@ int phy_class_info(const phy_ctx* ctx, long long* classes, int* levels, int* roo
   if (staged) *staged = e ? e->stage_sec : 0;
   if (tiles) *tiles = e ? e->ntiles : 0;
   if (spans) *spans = nspan;
+  return PHY_OK;
+}
+
+int phy_quad_plan(const phy_ctx* ctx, int* waves, int* span, int* slots) {
+  if (!ctx) return fail(PHY_EINVAL, "NULL ctx");
+  if (ctx->ms) return phy_quad_plan(ctx->ms->shard[0], waves, span, slots);
+  const bool on = ctx->qmw_ok && ctx->qmw_pref;
+  if (waves) *waves = on ? ctx->qmw_W : (ctx->quad_ok ? 1 : 0);
+  if (span) *span = on ? ctx->qmw_span : ctx->nsteps;
+  if (slots) *slots = on ? ctx->qmw_nslot : 0;
   return PHY_OK;
 }
 

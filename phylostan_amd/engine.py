@@ -349,6 +349,14 @@ class TreeLikelihood:
                     clades=nc.value, clade_max=big.value, chain_levels=cl.value, chain_lowest=clo.value,
                     chain_top_classes=ctop.value)
 
+    def quad_plan(self):
+        """The small-call sweep's plan: waves per category, schedule length in
+        program steps, LDS hand-off slots (include/phylo_hip.h phy_quad_plan)."""
+        w, sp, sl = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
+        _lib.check(self.lib.phy_quad_plan(self.ctx, ctypes.byref(w), ctypes.byref(sp), ctypes.byref(sl)),
+                   "phy_quad_plan")
+        return dict(waves=w.value, span=sp.value, slots=sl.value)
+
     def timing_start(self):
         _lib.check(self.lib.phy_timing_start(self.ctx), "phy_timing_start")
 

@@ -181,6 +181,11 @@ def test_quad_multiwave_rows_bitwise_equal_one_wave(name, n, monkeypatch):
     for qmw in ("0", "1"):
         monkeypatch.setenv("PHY_QMW", qmw)
         eng = _engine(case, max_draws=n, monkeypatch=monkeypatch)
+        plan = eng.quad_plan()
+        if qmw == "0":
+            assert plan["waves"] == 1 and plan["span"] == case.S - 1
+        elif case.C <= 4:
+            assert plan["waves"] >= 2 and plan["span"] < case.S - 1, plan
         out[qmw] = eng.evaluate_rows(bl, mv)
         if n == 1:
             out[qmw + "s"] = eng.evaluate(case.blens, case.model_vec(), site_ll=True).site_ll
