@@ -185,7 +185,9 @@ def test_quad_multiwave_rows_bitwise_equal_one_wave(name, n, monkeypatch):
         if qmw == "0":
             assert plan["waves"] == 1 and plan["span"] == case.S - 1
         elif case.C <= 4:
-            assert plan["waves"] >= 2 and plan["span"] < case.S - 1, plan
+            assert plan["waves"] >= 2 and plan["span"] <= case.S - 1, plan
+            if name in ("fluA", "HCV", "balanced"):  # (a caterpillar has nothing to run side by side)
+                assert plan["span"] < 0.75 * (case.S - 1), plan
         out[qmw] = eng.evaluate_rows(bl, mv)
         if n == 1:
             out[qmw + "s"] = eng.evaluate(case.blens, case.model_vec(), site_ll=True).site_ll
