@@ -2207,6 +2207,7 @@ struct phy_ctx {
   bool klat = false;           // K = 1 latency plan (sweep_kernel<512, 1, .>: no register spills)
   bool klat_pref = true;       // PHY_KLAT=0: the latency plan keeps the four-wave K = 1 kernel
   bool eig_fuse_pref = true;   // PHY_EIG_FUSE=0: small device batches take eig_kernel + pmat_kernel<false>
+  int eig_fuse_max = EIG_FUSE_MAX;  // PHY_EIG_FUSE_MAX: draws per launch up to which pmat_kernel forms them
   // the quad sweep (quad_engine.inc) for calls of <= QUAD_MAX_DRAWS draws
   bool quad_pref = true;       // PHY_QUAD=0: off
   // the multi-wave quad sweep (qmw_kernel): W waves per category share a block
@@ -2917,7 +2918,7 @@ int launch(phy_ctx* ctx, int n, const double* d_blens, const double* d_model, do
     // eigensystems: given (host-formed, the small host-buffer path); small
     // device batches: each pmat wave forms its draw's (one launch less);
     // large ones: one thread per draw first
-    const int with_eig = (!d_eig_in && n <= EIG_FUSE_MAX && ctx->eig_fuse_pref) ? 1 : 0;
+    const int with_eig = (!d_eig_in && n <= ctx->eig_fuse_max && ctx->eig_fuse_pref) ? 1 : 0;
     PmatArgs pa{d_model, d_blens, ctx->d_mat_branch, const_cast<double*>(ctx->eig_cur), ctx->d_pmat, C, B, ctx->kind,
                 ctx->nmat, n, ctx->R, ctx->extra, with_eig};
     if (!with_eig && !d_eig_in) {
@@ -3312,6 +3313,7 @@ int phy_create(int S, int P, int C, int rooted, int model, const uint8_t* tipcod
     const char* lk = getenv("PHY_KLAT");
     c->klat_pref = lk ? atoi(lk) != 0 : true;
     c->eig_fuse_pref = env_flag("PHY_EIG_FUSE", 1);
+    if (const char* em = getenv("PHY_EIG_FUSE_MAX")) c->eig_fuse_max = std::max(0, atoi(em));
     const char* qk2 = getenv("PHY_QUAD");
     c->quad_pref = qk2 ? atoi(qk2) != 0 : true;
     const char* qm = getenv("PHY_QMW");
