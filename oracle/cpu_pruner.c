@@ -36,10 +36,15 @@ static void jacobi_rot(double app, double aqq, double apq, double* cs, double* s
     *sn = 0.0;
     return;
   }
-  double theta = (aqq - app) / (2.0 * apq);
-  double t = (theta >= 0.0 ? 1.0 : -1.0) / (fabs(theta) + sqrt(theta * theta + 1.0));
-  *cs = 1.0 / sqrt(t * t + 1.0);
-  *sn = t * *cs;
+  /* t = sgn(theta) / (|theta| + sqrt(theta^2 + 1)), theta = d / e, divisions
+   * folded: cs = den / w, sn = sgn(theta) |e| / w, den = |d| + sqrt(d^2 + e^2),
+   * w = sqrt(den^2 + e^2) (the device's jacobi_rot, operation for operation) */
+  const double d = aqq - app, e = 2.0 * apq;
+  const double den = fabs(d) + sqrt(d * d + e * e);
+  const double inv = 1.0 / sqrt(den * den + e * e);
+  const double ae = fabs(e);
+  *cs = den * inv;
+  *sn = ((d == 0.0 || (d > 0.0) == (e > 0.0)) ? ae : -ae) * inv;
 }
 
 static void jacobi4(double A[4][4], double V[4][4], double lam[4]) {

@@ -1358,8 +1358,8 @@ struct PmatArgs {
 // parallel ordering: each sweep is three rounds of two rotations on disjoint
 // index pairs -- {(0,1),(2,3)}, {(0,2),(1,3)}, {(0,3),(1,2)}.  A round's two
 // rotation parameters read entries the other rotation does not change, so
-// their chains (division, square root, division, square root, division: the
-// latency of the solve on one GPU thread) run side by side -- three chains
+// their chains (square root, square root, division: the latency of the
+// solve on one GPU thread) run side by side -- three chains
 // per sweep instead of six.  Then A <- J^T A J and V <- V J for the round's
 // combined rotation J.  No FMA contraction here or in eig_record, and every
 // operation in the C oracle's order (oracle/cpu_pruner.c jacobi4): the same
@@ -1372,10 +1372,16 @@ __host__ __device__ inline void jacobi_rot(double app, double aqq, double apq, d
     sn = 0.0;
     return;
   }
-  const double theta = (aqq - app) / (2.0 * apq);
-  const double t = (theta >= 0.0 ? 1.0 : -1.0) / (fabs(theta) + sqrt(theta * theta + 1.0));
-  cs = 1.0 / sqrt(t * t + 1.0);
-  sn = t * cs;
+  // t = sgn(theta) / (|theta| + sqrt(theta^2 + 1)), theta = d / e, with the
+  // divisions folded: cs = 1 / sqrt(t^2 + 1) = den / w, sn = t cs =
+  // sgn(theta) |e| / w, den = |d| + sqrt(d^2 + e^2), w = sqrt(den^2 + e^2)
+  // (two square roots and one division on the chain instead of three)
+  const double d = aqq - app, e = 2.0 * apq;
+  const double den = fabs(d) + sqrt(d * d + e * e);
+  const double inv = 1.0 / sqrt(den * den + e * e);
+  const double ae = fabs(e);
+  cs = den * inv;
+  sn = ((d == 0.0 || (d > 0.0) == (e > 0.0)) ? ae : -ae) * inv;  // sgn(theta): + at theta = 0
 }
 __host__ __device__ void jacobi4(double A[4][4], double V[4][4], double lam[4]) {
 #pragma clang fp contract(off)
