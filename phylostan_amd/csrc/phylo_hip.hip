@@ -2834,7 +2834,7 @@ int launch_class(phy_ctx* ctx, int n, const double* d_blens, const double* d_mod
     hipLaunchKernelGGL(cls_fwd_kernel, dim3((L.nchunk + CLS_WPG - 1) / CLS_WPG, dcn), dim3(CLS_THREADS), 0, st, a);
   }
   if (chain)  // levels lo..hi in one launch
-    hipLaunchKernelGGL(e->chain_m <= 4 ? cls_chain_fwd_kernel<4>
+    hipLaunchKernelGGL(e->chain_m <= 4 ? cls_chain_fwd_kernel<4> : e->chain_m == 5 ? cls_chain_fwd_kernel<5>
                        : e->chain_m <= 6 ? cls_chain_fwd_kernel<6> : cls_chain_fwd_kernel<CHAIN_MAX>,
                        dim3(chain_wgs, dcn), dim3(CLS_THREADS), 0, st, a, ca);
   if (!flow) {
@@ -2855,7 +2855,7 @@ int launch_class(phy_ctx* ctx, int n, const double* d_blens, const double* d_mod
                          (const int*)e->d_lfix + L.lfix0, L.nlfix);
     if (in_chain(l)) {  // the chain's levels: one reverse launch at its top (levels below hold no staged tiles)
       if (l == e->chain_hi)
-        hipLaunchKernelGGL(e->chain_m <= 4 ? cls_chain_rev_kernel<4>
+        hipLaunchKernelGGL(e->chain_m <= 4 ? cls_chain_rev_kernel<4> : e->chain_m == 5 ? cls_chain_rev_kernel<5>
                            : e->chain_m <= 6 ? cls_chain_rev_kernel<6> : cls_chain_rev_kernel<CHAIN_MAX>,
                            dim3(chain_wgs, dcn), dim3(CLS_THREADS), 0, st, a, ca);
       continue;
