@@ -176,7 +176,8 @@ step_multidev() {
 }
 step_prof() {
   timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof_fluA -o run -- \
-    python bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-sampler-latency > $O/prof_fluA.log 2>&1
+    python bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-sampler-latency --no-synthetic > $O/prof_fluA.log 2>&1
+  python tools/prof_stats.py $O/prof_fluA/run_results.db | head -6
 }
 step_lat() {  # small calls: quad sweep against the column sweeps (PHY_QUAD=0)
   for w in fluA HCV DS1; do
@@ -201,8 +202,8 @@ step_lat4() {  # the sampler's call only (4 draws), every engine, plus its kerne
     python tools/latency_probe.py --workload fluA --draws 4 --engine pattern > $O/prof_lat4.log 2>&1
   python tools/prof_stats.py $O/prof_lat4/run_results.db
 }
-step_sq4() {  # SQ counters of the quad sweep on the 4-draw fluA call (separate --pmc passes)
-  PMC_SCRIPT=tools/latency_probe.py PMC_KERNEL=qsweep timeout -k 10 600 python tools/pmc_sq.py \
+step_sq4() {  # SQ counters of the (multi-wave) quad sweep on the 4-draw fluA call (separate --pmc passes)
+  PMC_SCRIPT=tools/latency_probe.py PMC_KERNEL=qmw timeout -k 10 600 python tools/pmc_sq.py \
     --workload fluA --draws 4 --engine pattern --calls 50 > $O/sq4_qsweep.json 2> $O/sq4_qsweep.err
   PMC_SCRIPT=tools/latency_probe.py PMC_KERNEL=qfin timeout -k 10 600 python tools/pmc_sq.py \
     --workload fluA --draws 4 --engine pattern --calls 50 > $O/sq4_qfin.json 2> $O/sq4_qfin.err
@@ -232,7 +233,7 @@ step_profn() {  # kernel traces of the batched-draw class sweep (4 draws per cal
 }
 step_pmc() {  # HBM traffic (FETCH / WRITE passes) and SQ counters of the timed kernels, fluA and synthetic
   timeout -k 10 600 python tools/pmc_traffic.py --workload fluA > $O/pmc_traffic_fluA.log 2>&1 && tail -1 $O/pmc_traffic_fluA.log
-  timeout -k 10 600 python tools/pmc_sq.py --steps 3 --warmup 1 --no-cpu-baseline --no-sampler-latency \
+  timeout -k 10 600 python tools/pmc_sq.py --steps 3 --warmup 1 --no-cpu-baseline --no-sampler-latency --no-synthetic \
     > $O/sq_pattern_fluA.json 2> $O/sq_pattern_fluA.err && head -c 400 $O/sq_pattern_fluA.json
   timeout -k 10 600 python tools/pmc_traffic.py --workload synthetic --engine class > $O/pmc_traffic_synth.log 2>&1 \
     && tail -1 $O/pmc_traffic_synth.log

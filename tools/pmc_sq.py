@@ -21,7 +21,7 @@ PASSES = [
 
 
 def main():
-    bench_args = sys.argv[1:] or ["--steps", "3", "--warmup", "1", "--no-cpu-baseline"]
+    bench_args = sys.argv[1:] or ["--steps", "3", "--warmup", "1", "--no-cpu-baseline", "--no-synthetic"]
     out = {}
     for k, counters in enumerate(PASSES):
         d = os.path.join(ROOT, "gpurun_out", "pmc_sq", "p%d" % k)

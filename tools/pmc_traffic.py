@@ -26,8 +26,9 @@ sys.path.insert(0, ROOT)
 
 
 # the class sweep's timed region (phy_timing_*: forward through the last reverse level)
-CLASS_KERNELS = ("cls_clade_fwd_kernel", "cls_fwd_kernel", "cls_root_kernel", "cls_red_kernel", "cls_red_list_kernel",
-                 "cls_fix_list_kernel", "cls_rev_kernel", "cls_clade_rev_kernel")
+CLASS_KERNELS = ("cls_clade_fwd_kernel", "cls_fwd_kernel", "cls_chain_fwd_kernel", "cls_root_kernel", "cls_red_kernel",
+                 "cls_red_list_kernel", "cls_fix_list_kernel", "cls_rev_kernel", "cls_chain_rev_kernel",
+                 "cls_clade_rev_kernel")
 
 
 def run_pass(counter, out_dir, bench_args, engine):
@@ -67,7 +68,7 @@ def main():
     from bench import kernel_source_hash
     draws = args.draws or (1 if args.workload == "synthetic" else 8192)
     bench_args = ["--workload", args.workload, "--draws", str(draws), "--steps", "3", "--warmup", "1",
-                  "--no-cpu-baseline", "--no-sampler-latency", "--engine", args.engine]
+                  "--no-cpu-baseline", "--no-sampler-latency", "--no-synthetic", "--engine", args.engine]
     tag = "%s_%s" % (args.workload, args.engine)
     fetch, nf = run_pass("FETCH_SIZE", os.path.join(args.scratch, tag + "_fetch"), bench_args, args.engine)
     write, nw = run_pass("WRITE_SIZE", os.path.join(args.scratch, tag + "_write"), bench_args, args.engine)
