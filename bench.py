@@ -805,12 +805,12 @@ def main():
             rec = json.load(open(sqp))
             sq = rec.get("per_launch", {}).get("%s:pattern" % args.workload)
             if rec.get("kernel_source") == kernel_source_hash() and sq:
-                flops = 64.0 * (2.0 * sq["SQ_INSTS_VALU_FMA_F64"] + sq["SQ_INSTS_VALU_MUL_F64"]
-                                + sq["SQ_INSTS_VALU_ADD_F64"])
+                cflops = 64.0 * (2.0 * sq["SQ_INSTS_VALU_FMA_F64"] + sq["SQ_INSTS_VALU_MUL_F64"]
+                                 + sq["SQ_INSTS_VALU_ADD_F64"])  # counted, not SURVEY 8d's algorithmic flops
                 t = kern_avg_ms * 1e-3
                 simd_cycles = t * 2.4e9 * 1024  # 256 CUs x 4 SIMDs at 2.4 GHz
-                compute = {"fp64_tflops": flops / t / 1e12, "fp64_peak_tflops": PEAK_FP64_TFLOPS,
-                           "fp64_frac": flops / t / 1e12 / PEAK_FP64_TFLOPS,
+                compute = {"fp64_tflops": cflops / t / 1e12, "fp64_peak_tflops": PEAK_FP64_TFLOPS,
+                           "fp64_frac": cflops / t / 1e12 / PEAK_FP64_TFLOPS,
                            "valu_busy": 4.0 * sq["SQ_ACTIVE_INST_VALU"] / simd_cycles,
                            "instructions_per_wave": sq["SQ_INSTS"] / sq["SQ_WAVES"],
                            "source": "profiles/sq_counters.json (rocprofv3 --pmc SQ counters of this kernel source; "
