@@ -40,6 +40,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <climits>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -2828,9 +2829,15 @@ int launch_class(phy_ctx* ctx, int n, const double* d_blens, const double* d_mod
   auto in_chain = [&](int l) { return chain && l >= e->chain_lo && l <= e->chain_hi; };
   for (int l = e->Lc + 1; l < e->levels && !flow; ++l) {
     const ClassLevel& L = e->lv[l];
-    if (!L.nchunk || in_chain(l)) continue;
+    if (!L.nchunk || in_chain(l) || L.pair == 2) continue;
     a.first = L.chunk0;
     a.count = L.nchunk;
+    if (L.pair == 1) {  // this level and the next (its chunks follow): cls_fwd2_kernel
+      a.count += e->lv[l + 1].nchunk;
+      hipLaunchKernelGGL(cls_fwd2_kernel, dim3((a.count + CLS_WPG - 1) / CLS_WPG, dcn), dim3(CLS_THREADS), 0, st, a,
+                         (const int2*)e->d_pair, (const int4*)e->d_gc);
+      continue;
+    }
     hipLaunchKernelGGL(cls_fwd_kernel, dim3((L.nchunk + CLS_WPG - 1) / CLS_WPG, dcn), dim3(CLS_THREADS), 0, st, a);
   }
   if (chain)  // levels lo..hi in one launch
@@ -3974,6 +3981,13 @@ int phy_class_chain(const phy_ctx* ctx, int* levels, int* lowest, int* top_class
   if (levels) *levels = e ? e->chain_m : 0;
   if (lowest) *lowest = e && e->chain_m ? e->chain_lo : 0;
   if (top_classes) *top_classes = e ? e->chain_ntop : 0;
+  return PHY_OK;
+}
+
+int phy_class_pairs(const phy_ctx* ctx, int* pairs) {
+  if (!ctx) return fail(PHY_EINVAL, "NULL ctx");
+  if (ctx->ms) return phy_class_pairs(ctx->ms->shard[0], pairs);
+  if (pairs) *pairs = ctx->ce ? ctx->ce->npairs : 0;
   return PHY_OK;
 }
 

@@ -325,3 +325,64 @@ def test_class_chain_batched_draws_and_repeats(monkeypatch):
     one = _class_engine(case, max_draws=1)
     for k in (0, 7, 15):
         assert np.array_equal(one.evaluate_rows(bl[k:k + 1], mv[k:k + 1])[0], rows[k])
+
+
+def _pair_engines(case, monkeypatch, max_draws=1, pmax=None):
+    """The same plan with forward level pairs (PHY_PAIR_MAX=pmax, or the
+    default) and without (PHY_PAIR=0)."""
+    monkeypatch.setenv("PHY_PAIR", "0")
+    plain = _class_engine(case, max_draws=max_draws)
+    monkeypatch.delenv("PHY_PAIR")
+    if pmax is not None:
+        monkeypatch.setenv("PHY_PAIR_MAX", str(pmax))
+    paired = _class_engine(case, max_draws=max_draws)
+    monkeypatch.delenv("PHY_PAIR_MAX", raising=False)
+    assert plain.class_info()["level_pairs"] == 0
+    return paired, plain
+
+
+@pytest.mark.parametrize("make", [cases.fluA_case, cases.hcv_case, cases.ds1_case, "syn200k", "caterpillar", "deep"],
+                         ids=["fluA", "HCV", "DS1_unrooted", "synthetic200k", "caterpillar_random", "random300"])
+@pytest.mark.parametrize("pmax", [None, 1 << 40], ids=["default", "all"])
+def test_class_level_pairs_bitwise_equal_to_level_launches(make, pmax, monkeypatch):
+    """Forward level pairs (cls_fwd2_kernel: two levels in one launch, the
+    upper level recomputing its lower-level children from their children with
+    the lower level's own arithmetic) leave every output bitwise equal to the
+    per-level launches; at the parity bar against the oracle."""
+    if make == "syn200k":
+        from phylostan_amd import synthetic
+        pd, prm = synthetic.simulate(n_sites=200_000)
+        case = cases.Case("syn200k", pd.tipcodes, pd.weights, pd.peel0, True, "GTR", 4, prm["blens"], prm["freqs"],
+                          prm["rates"], prm["rs"], prm["ps"])
+    elif make == "caterpillar":
+        case = cases.random_case(5, S=40, P=2000, C=3, model="GTR", rooted=True, caterpillar=True)
+    elif make == "deep":
+        case = cases.random_case(9, S=300, P=500, C=4, model="GTR", rooted=True)
+    else:
+        case = make()
+    if pmax is not None:  # every level launched on its own (no clade, no chain), all of them paired
+        monkeypatch.setenv("PHY_CLADE", "0")
+        monkeypatch.setenv("PHY_CHAIN", "0")
+    paired, plain = _pair_engines(case, monkeypatch, pmax=pmax)
+    if pmax is not None:
+        info = paired.class_info()
+        assert info["level_pairs"] == (info["levels"] - 1) // 2, info
+    a = paired.evaluate(case.blens, case.model_vec(), site_ll=True)
+    b = plain.evaluate(case.blens, case.model_vec(), site_ll=True)
+    _assert_rows_equal(a, b)
+    check_case(case, paired, a)
+
+
+def test_class_level_pairs_batched_draws_and_repeats(monkeypatch):
+    """Paired plan, 8 draws per launch: rows bitwise equal to the unpaired
+    plan's, and repeated launches bitwise reproducible."""
+    case = cases.random_case(9, S=300, P=500, C=4, model="GTR", rooted=True)
+    monkeypatch.setenv("PHY_CLADE", "0")
+    paired, plain = _pair_engines(case, monkeypatch, max_draws=8, pmax=1 << 40)
+    assert paired.class_info()["level_pairs"] >= 2
+    rng = np.random.default_rng(5)
+    bl = case.blens[None, :] * rng.uniform(0.7, 1.3, (8, case.blens.size))
+    mv = np.repeat(case.model_vec()[None], 8, axis=0)
+    rows = paired.evaluate_rows(bl, mv)
+    assert np.array_equal(rows, plain.evaluate_rows(bl, mv))
+    assert np.array_equal(rows, paired.evaluate_rows(bl, mv))
