@@ -279,13 +279,17 @@ int phy_class_clades(const phy_ctx* ctx, int* fused_levels, int* clades, long lo
  * A plan with a chain has no dataflow launch (phy_set_flow has no effect). */
 int phy_class_chain(const phy_ctx* ctx, int* levels, int* lowest, int* top_classes);
 
-/* Forward level pairs of the class sweep: pairs of adjacent levels (above the
- * fused clade levels, below the top chain) whose forward passes run as one
- * launch, the upper level recomputing its children of the level below from
- * theirs -- bitwise the per-level values.  PHY_PAIR=0 (read at phy_create)
- * plans none; PHY_PAIR_MAX=n pairs only levels whose upper level holds at
- * most n classes (default: no cap). */
-int phy_class_pairs(const phy_ctx* ctx, int* pairs);
+/* Launch fusions of the class sweep's level launches, both bitwise the
+ * unfused values (read at phy_create):
+ *   level_pairs   forward level pairs -- adjacent levels (above the fused
+ *                 clade levels, below the top chain) in one launch, the upper
+ *                 level recomputing its children of the level below from
+ *                 theirs.  PHY_PAIR=0: none; PHY_PAIR_MAX=n: only upper
+ *                 levels of at most n classes (default: no cap).
+ *   chunk_spans   long tile-crossing segments summed by the reverse chunk
+ *                 of their class (the whole wave), so those levels have no
+ *                 FIX launch.  PHY_REVFIX=0: none. */
+int phy_class_fused(const phy_ctx* ctx, int* level_pairs, int* chunk_spans);
 
 /* The sampler's small-call sweep (calls of <= 16 draws, the quad sweep):
  * waves per category (0: the quad sweep does not apply to this context, 1:

@@ -2857,7 +2857,7 @@ int launch_class(phy_ctx* ctx, int n, const double* d_blens, const double* d_mod
       a.sfirst = L.sec0;
       hipLaunchKernelGGL(cls_red_kernel, dim3((L.ntile + CLS_WPG - 1) / CLS_WPG, dcn), dim3(CLS_THREADS), 0, st, a);
     }
-    if (L.nlfix)  // the level's long spans (the short ones are summed by the REV lanes)
+    if (L.nlfix && !L.revfix)  // the level's long spans (the short ones are summed by the REV lanes)
       hipLaunchKernelGGL(cls_fix_list_kernel, dim3((L.nlfix + CLS_WPG - 1) / CLS_WPG, dcn), dim3(CLS_THREADS), 0, st, a,
                          (const int*)e->d_lfix + L.lfix0, L.nlfix);
     if (in_chain(l)) {  // the chain's levels: one reverse launch at its top (levels below hold no staged tiles)
@@ -2870,7 +2870,11 @@ int launch_class(phy_ctx* ctx, int n, const double* d_blens, const double* d_mod
     if (L.nchunk) {
       a.first = L.chunk0;
       a.count = L.nchunk;
-      hipLaunchKernelGGL(cls_rev_kernel, dim3((L.nchunk + CLS_WPG - 1) / CLS_WPG, dcn), dim3(CLS_THREADS), 0, st, a);
+      if (L.revfix)  // ... the long ones by the chunks' waves
+        hipLaunchKernelGGL(cls_rev_ls_kernel, dim3((L.nchunk + CLS_WPG - 1) / CLS_WPG, dcn), dim3(CLS_THREADS), 0, st, a,
+                           (const int2*)e->d_clf, (const int*)e->d_clong);
+      else
+        hipLaunchKernelGGL(cls_rev_kernel, dim3((L.nchunk + CLS_WPG - 1) / CLS_WPG, dcn), dim3(CLS_THREADS), 0, st, a);
     }
   }
   if (!flow && e->Lc > 0) {
@@ -3984,10 +3988,11 @@ int phy_class_chain(const phy_ctx* ctx, int* levels, int* lowest, int* top_class
   return PHY_OK;
 }
 
-int phy_class_pairs(const phy_ctx* ctx, int* pairs) {
+int phy_class_fused(const phy_ctx* ctx, int* level_pairs, int* chunk_spans) {
   if (!ctx) return fail(PHY_EINVAL, "NULL ctx");
-  if (ctx->ms) return phy_class_pairs(ctx->ms->shard[0], pairs);
-  if (pairs) *pairs = ctx->ce ? ctx->ce->npairs : 0;
+  if (ctx->ms) return phy_class_fused(ctx->ms->shard[0], level_pairs, chunk_spans);
+  if (level_pairs) *level_pairs = ctx->ce ? ctx->ce->npairs : 0;
+  if (chunk_spans) *chunk_spans = ctx->ce ? ctx->ce->nclong : 0;
   return PHY_OK;
 }
 

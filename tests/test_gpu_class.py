@@ -386,3 +386,50 @@ def test_class_level_pairs_batched_draws_and_repeats(monkeypatch):
     rows = paired.evaluate_rows(bl, mv)
     assert np.array_equal(rows, plain.evaluate_rows(bl, mv))
     assert np.array_equal(rows, paired.evaluate_rows(bl, mv))
+
+
+def _repetitive_case(seed=70, S=48, P=5000):
+    """A repetitive alignment: long tile-crossing segments (one class of a
+    small node collecting most of its parent's classes)."""
+    rng = np.random.default_rng(seed)
+    base = cases.random_case(seed, S=S, P=P, C=4, model="GTR")
+    codes = np.where(rng.random((S, P)) < 0.9, 1, rng.choice([1, 2, 4, 8, 15], size=(S, P)))
+    return cases.Case("rep", codes.astype(np.uint8), base.weights, base.peel0, True, "GTR", 4, base.blens,
+                      base.freqs, base.rates, base.rs, base.ps)
+
+
+@pytest.mark.parametrize("make", ["rep", "rep_noclade", "rep_nochain", cases.fluA_case, "syn200k"],
+                         ids=["repetitive", "repetitive_no_clades", "repetitive_no_chain", "fluA", "synthetic200k"])
+def test_class_revfix_bitwise_equal_to_fix_launches(make, monkeypatch):
+    """Long tile-crossing segments summed by their REV chunk's wave
+    (cls_rev_ls_kernel, fix_span's arithmetic) instead of a FIX launch per
+    level: every output bitwise equal, batched draws too."""
+    if make == "syn200k":
+        from phylostan_amd import synthetic
+        pd, prm = synthetic.simulate(n_sites=200_000)
+        case = cases.Case("syn200k", pd.tipcodes, pd.weights, pd.peel0, True, "GTR", 4, prm["blens"], prm["freqs"],
+                          prm["rates"], prm["rs"], prm["ps"])
+    elif isinstance(make, str):
+        case = _repetitive_case()
+        if make == "rep_noclade":
+            monkeypatch.setenv("PHY_CLADE", "0")
+        if make == "rep_nochain":
+            monkeypatch.setenv("PHY_CLADE", "0")
+            monkeypatch.setenv("PHY_CHAIN", "0")
+    else:
+        case = make()
+    monkeypatch.setenv("PHY_REVFIX", "0")
+    plain = _class_engine(case, max_draws=3)
+    monkeypatch.delenv("PHY_REVFIX")
+    fused = _class_engine(case, max_draws=3)
+    if isinstance(make, str) and make.startswith("rep_no"):
+        assert fused.class_info()["chunk_spans"] > 0, fused.class_info()
+    assert plain.class_info()["chunk_spans"] == 0
+    a = fused.evaluate(case.blens, case.model_vec(), site_ll=True)
+    b = plain.evaluate(case.blens, case.model_vec(), site_ll=True)
+    _assert_rows_equal(a, b)
+    check_case(case, fused, a)
+    rng = np.random.default_rng(8)
+    bl = case.blens[None, :] * rng.uniform(0.8, 1.2, (3, case.blens.size))
+    mv = np.repeat(case.model_vec()[None], 3, axis=0)
+    assert np.array_equal(fused.evaluate_rows(bl, mv), plain.evaluate_rows(bl, mv))
