@@ -26,8 +26,8 @@ sys.path.insert(0, ROOT)
 
 
 # the class sweep's timed region (phy_timing_*: forward through the last reverse level)
-CLASS_KERNELS = ("cls_clade_fwd_kernel", "cls_fwd_kernel", "cls_chain_fwd_kernel", "cls_root_kernel", "cls_red_kernel",
-                 "cls_red_list_kernel", "cls_fix_list_kernel", "cls_rev_kernel", "cls_chain_rev_kernel",
+CLASS_KERNELS = ("cls_clade_fwd_kernel", "cls_fwd_kernel", "cls_fwd2_kernel", "cls_chain_fwd_kernel", "cls_root_kernel", "cls_red_kernel",
+                 "cls_red_list_kernel", "cls_fix_list_kernel", "cls_rev_kernel", "cls_rev_ls_kernel", "cls_chain_rev_kernel",
                  "cls_clade_rev_kernel")
 
 
