@@ -543,7 +543,8 @@ class Posterior:
                 tok["done"] = e.value
                 return tok
             tok["gen"] = gen
-            if hasattr(self.lik, "submit_rows") and req[0].shape[0] <= 64:
+            if hasattr(self.lik, "submit_rows") and req[0].shape[0] <= min(getattr(self.lik, "max_draws", 64),
+                                                                            getattr(self.lik, "_STAGE_DRAWS", 64)):
                 self.lik.submit_rows(*req)
                 tok["async"] = True
             else:
