@@ -1505,7 +1505,6 @@ __device__ void eig_record_wave(const double* mdl, int kind, double* out, double
   const bool own = lane < 16;
   double* A = sh;       // [4][4]
   double* V = sh + 16;  // [4][4]
-  double* T = sh + 32;  // scratch [4][4]
   if (kind == PHY_JC69) {
     if (own) out[EIG_Q + j * 4 + k] = (j == k) ? -1.0 : 1.0 / 3.0;
     __syncthreads();
@@ -1578,18 +1577,21 @@ __device__ void eig_record_wave(const double* mdl, int kind, double* out, double
         const double bv = by_col ? M[row * 4 + qq] : M[qq * 4 + col];
         return x == p ? cc * av - ss * bv : ss * av + cc * bv;
       };
+      // A <- J^T (A J): the two column-rotated entries of k's column that
+      // row j's rotation combines, (A J)[p][k] and (A J)[q][k] ({p, q} = j's
+      // pair), formed by this lane from A itself -- the same operations as
+      // the two-pass form, without the intermediate's LDS round trip and barrier
       double na = 0.0, nv = 0.0;
       if (own) {
-        na = rot(A, j, k, true);   // A <- A J (columns)
-        nv = rot(V, j, k, true);   // V <- V J
-        T[j * 4 + k] = na;
-      }
-      __syncthreads();
-      if (own) {
-        na = rot(T, j, k, false);  // A <- J^T A (rows)
+        const bool first = j == p1 || j == q1;
+        const int p = first ? p1 : p2, qq = first ? q1 : q2;
+        const double cc = first ? c1 : c2, ss = first ? s1 : s2;
+        const double tp = rot(A, p, k, true), tq = rot(A, qq, k, true);  // (A J)[p][k], (A J)[qq][k]
+        na = j == p ? cc * tp - ss * tq : ss * tp + cc * tq;
         if ((j == p1 && k == q1) || (j == q1 && k == p1) || (j == p2 && k == q2) || (j == q2 && k == p2)) na = 0.0;
+        nv = rot(V, j, k, true);   // V <- V J
       }
-      __syncthreads();
+      __syncthreads();  // every lane has read A and V
       if (own) {
         A[j * 4 + k] = na;
         V[j * 4 + k] = nv;
