@@ -2842,14 +2842,24 @@ int launch_class(phy_ctx* ctx, int n, const double* d_blens, const double* d_mod
     }
     hipLaunchKernelGGL(cls_fwd_kernel, dim3((L.nchunk + CLS_WPG - 1) / CLS_WPG, dcn), dim3(CLS_THREADS), 0, st, a);
   }
-  if (chain)  // levels lo..hi in one launch
+  // the root recomputes the chain's top (cls_root_kernel<·, ·, MC>) instead of
+  // a chain forward launch storing it (PHY_ROOT_CHAIN=0 at phy_create: the launch)
+  const bool root_chain = chain && C <= 4 && e->root_chain_pref;
+  if (chain && !root_chain)  // levels lo..hi in one launch
     hipLaunchKernelGGL(e->chain_m <= 4 ? cls_chain_fwd_kernel<4> : e->chain_m == 5 ? cls_chain_fwd_kernel<5>
                        : e->chain_m <= 6 ? cls_chain_fwd_kernel<6> : cls_chain_fwd_kernel<CHAIN_MAX>,
                        dim3(chain_wgs, dcn), dim3(CLS_THREADS), 0, st, a, ca);
   if (!flow) {
     auto rk = C <= 4 ? (e->root_tips ? cls_root_kernel<256, true> : cls_root_kernel<256, false>)
                      : (e->root_tips ? cls_root_kernel<1024, true> : cls_root_kernel<1024, false>);
-    hipLaunchKernelGGL(rk, dim3(e->nrootch, n), dim3(C * WAVE), 0, st, a);
+    if (root_chain) {
+      const int m = e->chain_m;
+      rk = e->root_tips ? (m <= 4 ? cls_root_kernel<256, true, 4> : m == 5 ? cls_root_kernel<256, true, 5>
+                           : m <= 6 ? cls_root_kernel<256, true, 6> : cls_root_kernel<256, true, CHAIN_MAX>)
+                        : (m <= 4 ? cls_root_kernel<256, false, 4> : m == 5 ? cls_root_kernel<256, false, 5>
+                           : m <= 6 ? cls_root_kernel<256, false, 6> : cls_root_kernel<256, false, CHAIN_MAX>);
+    }
+    hipLaunchKernelGGL(rk, dim3(e->nrootch, n), dim3(C * WAVE), 0, st, a, ca);
   }
   for (int l = e->levels - 1; l > e->Lc && !flow; --l) {
     const ClassLevel& L = e->lv[l];

@@ -433,3 +433,29 @@ def test_class_revfix_bitwise_equal_to_fix_launches(make, monkeypatch):
     bl = case.blens[None, :] * rng.uniform(0.8, 1.2, (3, case.blens.size))
     mv = np.repeat(case.model_vec()[None], 3, axis=0)
     assert np.array_equal(fused.evaluate_rows(bl, mv), plain.evaluate_rows(bl, mv))
+
+
+@pytest.mark.parametrize("make", [cases.fluA_case, cases.hcv_case, "syn200k"], ids=["fluA", "HCV", "synthetic200k"])
+def test_class_root_chain_bitwise_equal_to_chain_forward_launch(make, monkeypatch):
+    """The root recomputing the chain's top from the chain tables (no chain
+    forward launch) gives every output bitwise equal to the plan that stores
+    the chain's A in its own launch (PHY_ROOT_CHAIN=0), batched draws too."""
+    if make == "syn200k":
+        from phylostan_amd import synthetic
+        pd, prm = synthetic.simulate(n_sites=200_000)
+        case = cases.Case("syn200k", pd.tipcodes, pd.weights, pd.peel0, True, "GTR", 4, prm["blens"], prm["freqs"],
+                          prm["rates"], prm["rs"], prm["ps"])
+    else:
+        case = make()
+    monkeypatch.setenv("PHY_ROOT_CHAIN", "0")
+    plain = _class_engine(case, max_draws=3)
+    monkeypatch.delenv("PHY_ROOT_CHAIN")
+    fused = _class_engine(case, max_draws=3)
+    assert fused.class_info()["chain_levels"] >= 2
+    a = fused.evaluate(case.blens, case.model_vec(), site_ll=True)
+    b = plain.evaluate(case.blens, case.model_vec(), site_ll=True)
+    _assert_rows_equal(a, b)
+    rng = np.random.default_rng(12)
+    bl = case.blens[None, :] * rng.uniform(0.8, 1.2, (3, case.blens.size))
+    mv = np.repeat(case.model_vec()[None], 3, axis=0)
+    assert np.array_equal(fused.evaluate_rows(bl, mv), plain.evaluate_rows(bl, mv))
