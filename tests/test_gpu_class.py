@@ -279,8 +279,10 @@ def _chain_pair(case, monkeypatch, max_draws=1):
     return chained, plain
 
 
-@pytest.mark.parametrize("make", [cases.fluA_case, cases.hcv_case, cases.ds1_case, "syn200k", "caterpillar"],
-                         ids=["fluA", "HCV", "DS1_unrooted", "synthetic200k", "caterpillar_random"])
+@pytest.mark.parametrize("make", [cases.fluA_case, cases.hcv_case, cases.ds1_case, "syn200k", "caterpillar",
+                                  "caterpillar_c5"],
+                         ids=["fluA", "HCV", "DS1_unrooted", "synthetic200k", "caterpillar_random",
+                              "caterpillar_C5_chain_launch"])
 def test_class_chain_equals_level_launches(make, monkeypatch):
     """The top chain (the single-node levels below the root in one forward and
     one reverse launch, one lane per top class) forms the level launches'
@@ -295,6 +297,8 @@ def test_class_chain_equals_level_launches(make, monkeypatch):
                           prm["rates"], prm["rs"], prm["ps"])
     elif make == "caterpillar":
         case = cases.random_case(5, S=40, P=2000, C=3, model="GTR", rooted=True, caterpillar=True)
+    elif make == "caterpillar_c5":  # C > 4: the chain's own forward launch (the root recompute is C <= 4)
+        case = cases.random_case(6, S=40, P=2000, C=5, model="GTR", rooted=True, caterpillar=True)
     else:
         case = make()
     chained, plain = _chain_pair(case, monkeypatch)
