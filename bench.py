@@ -76,6 +76,9 @@ def parse():
                     help="parameter points per step of the synthetic sub-record")
     ap.add_argument("--no-multidev", action="store_true",
                     help="skip the phy_create_multi leg of the synthetic sub-record under --gpus N > 1")
+    ap.add_argument("--compact", action="store_true",
+                    help="compact output rows (log-lik + every parameter gradient, no dL/dP block): the rows a "
+                         "sampler consumes, and the payload of any reduction of them")
     ap.add_argument("--rehearse", action="store_true",
                     help="N > 1 rehearsal on a one-GPU box: every rank on device 0, gloo instead of RCCL for the "
                          "collectives (the line says so); checks the multi-rank path, measures nothing")
@@ -309,7 +312,7 @@ def multidev_child(n, steps, warmup, sites, draws, timeout=300):
     os.close(fd)
     cmd = [sys.executable, os.path.abspath(__file__), "--workload", "synthetic", "--multi-device", str(n),
            "--steps", str(steps), "--warmup", str(warmup), "--sites", str(sites), "--draws", str(draws),
-           "--no-cpu-baseline", "--json-out", path]
+           "--no-cpu-baseline", "--compact", "--json-out", path]
     t0 = time.perf_counter()
     try:
         cp = subprocess.run(cmd, env=env, timeout=timeout, stdout=subprocess.PIPE, stderr=subprocess.PIPE)
@@ -318,7 +321,7 @@ def multidev_child(n, steps, warmup, sites, draws, timeout=300):
         if cp.returncode != 0 or not txt:
             return dict(ok=False, returncode=cp.returncode, stderr_tail=cp.stderr.decode(errors="replace")[-600:])
         sub = json.loads(txt.splitlines()[-1])
-        keep = ("value", "unit", "n_gpus", "ms_per_step", "steps", "warmup", "nominal_loglik")
+        keep = ("value", "unit", "n_gpus", "ms_per_step", "steps", "warmup", "nominal_loglik", "row_doubles")
         out = {k: sub.get(k) for k in keep}
         out["devices"] = sub["config"].get("devices")
         out["reduction"] = sub["config"].get("reduction")
@@ -353,8 +356,11 @@ def synthetic_leg(args, world, rank, local, dev, cpu_group):
     S, P = prob["tipcodes"].shape
     C = prob["C"]
     draws = max(1, args.synthetic_draws)
+    # compact rows: log-lik and every parameter gradient (branch lengths, rates, mixture weights,
+    # exchangeabilities, frequencies) -- a sampler's whole gradient -- without the dL/dP block, so the
+    # step's one collective carries ~2 KB per draw instead of ~130 KB
     sl = ShardedLikelihood(prob["tipcodes"], prob["weights"], prob["peel0"], prob["rooted"], prob["model"], C,
-                           rank, world, device=local, max_draws=draws)
+                           rank, world, device=local, max_draws=draws, compact=True)
     eng = sl.engine
     info = {"engine": eng.engine()}
     if info["engine"] == "class":
@@ -407,13 +413,21 @@ def synthetic_leg(args, world, rank, local, dev, cpu_group):
     kern_ms, nl = eng.timing_read()
     kern_avg_ms = max_over_ranks(kern_ms / max(nl, 1))
     allreduce = None
-    if world > 1:  # the step's one collective alone: the full fp64 rows, ~130 KB per draw
-        buf = torch.zeros_like(d_out)
-        with torch.cuda.stream(stream):
-            for _ in range(5):
-                dist.all_reduce(buf)
-            ar = timed(lambda k: dist.all_reduce(buf), 50)
-        allreduce = dict(us_per_call=1e6 * ar / 50, bytes=buf.numel() * 8, op="all_reduce(SUM) fp64, %s" % ("RCCL" if dist.get_backend() == "nccl" else dist.get_backend()))
+    if world > 1:  # the step's one collective alone (its payload: the compact rows), and the full rows beside it
+        full_len = eng.outlen + 16 * C * B
+        op = "all_reduce(SUM) fp64, %s" % ("RCCL" if dist.get_backend() == "nccl" else dist.get_backend())
+        allreduce = dict(op=op, payload="compact rows: log-lik + every parameter gradient, %d doubles per draw "
+                                        "(the full rows' dL/dP block, %d doubles, is not reduced)"
+                                        % (eng.outlen, 16 * C * B))
+        for name, cols in (("compact", eng.outlen), ("full_rows", full_len)):
+            buf = torch.zeros((draws, cols), device=dev, dtype=torch.float64)
+            with torch.cuda.stream(stream):
+                for _ in range(5):
+                    dist.all_reduce(buf)
+                ar = timed(lambda k: dist.all_reduce(buf), 50)
+            allreduce[name] = dict(us_per_call=1e6 * ar / 50, bytes=buf.numel() * 8)
+        allreduce["us_per_call"] = allreduce["compact"]["us_per_call"]
+        allreduce["bytes"] = allreduce["compact"]["bytes"]
     step(0)  # parameter set 0, draw 0: the nominal point
     torch.cuda.synchronize(dev)
     row0 = d_out[0].double().cpu().numpy()
@@ -432,10 +446,12 @@ def synthetic_leg(args, world, rank, local, dev, cpu_group):
     rec = None
     if rank == 0:
         hinfo = host_cpu_info()
-        cpu = None
+        cpu = cpu_mt = None
         if world == 1 and not args.no_cpu_baseline:
-            # bounded sample: ONE full evaluation of the whole alignment, one thread (~10-20 s)
+            # bounded sample: ONE full evaluation of the whole alignment, one thread (~7 s)
             cpu, ref = cpu_baseline(prob, 0.0, info=hinfo)
+            if hinfo["threads"] > 1:  # ... and one on every host thread this job may use (OpenMP over patterns)
+                cpu_mt, _ = cpu_baseline(prob, 0.0, nthreads=hinfo["threads"], info=hinfo)
         else:  # the check only: the C port on every host thread this job may use
             from oracle import cpu as ocpu
             from phylostan_amd import models
@@ -480,9 +496,11 @@ def synthetic_leg(args, world, rank, local, dev, cpu_group):
                          else "sweep_kernel",
                          "kernel_avg_ms": kern_avg_ms, "algorithmic_bytes_per_launch": alg,
                          "survey_model_bytes_per_launch": survey_bytes(S, sl.p1 - sl.p0, C, draws),
+                         "hbm": counted_hbm(traffic, alg, kern_avg_ms),
                          "limiter": "latency / launch chain: dependent kernels per tree level (DESIGN.md 5b)"},
             "allreduce": allreduce,
             "cpu_baseline": cpu,
+            "cpu_baseline_all_threads": cpu_mt,
             "nominal_check": check,
             "multidev": multidev,
             "program": info,
@@ -492,6 +510,21 @@ def synthetic_leg(args, world, rank, local, dev, cpu_group):
         dist.barrier(group=cpu_group)
     eng.close()
     return rec
+
+
+def counted_hbm(traffic, alg, kern_avg_ms):
+    """The rocprof-counted HBM rate of the dominant kernel: PMC bytes per
+    launch (profiles/pmc_traffic.json, this kernel source) over the launch's
+    average duration, and its fraction of the 8 TB/s peak; None-valued when
+    no PMC record of this source exists."""
+    if not traffic:
+        return {"counted_gbps": None, "counted_frac": None, "traffic_over_algorithmic": None, "counted_note": None}
+    g = traffic / (kern_avg_ms * 1e-3) / 1e9
+    note = ("counted bytes below the algorithmic count: reuse in L2 / MALL (the small gathers of class vectors "
+            "hit cache)" if traffic < alg else
+            "counted bytes above the algorithmic count: re-read / re-staged bytes (DESIGN.md 7)")
+    return {"counted_gbps": g, "counted_frac": g / PEAK_HBM_GBPS, "traffic_over_algorithmic": traffic / alg,
+            "counted_note": note}
 
 
 def pmc_record(workload, draws, engine):
@@ -536,10 +569,7 @@ def main():
 
     cpu_group = None
     if args.rehearse:
-        local = 0
-        # the ranks share one GPU: the class sweep's dataflow launch wants its grid resident, so the
-        # rehearsal takes the level launches (phy_set_flow); the multidev child inherits this
-        os.environ["PHY_FLOW"] = "0"
+        local = 0  # the ranks share one GPU
     if world > 1:
         torch.cuda.set_device(local)
         if args.rehearse:
@@ -605,6 +635,8 @@ def main():
     if args.shard_of > 1:
         sl.world = 1  # the projection: one shard's evaluation, no collective
     eng = sl.engine
+    if args.compact:
+        eng.set_output(compact=True)
     if args.engine != "auto":
         eng.set_engine(args.engine)
     if args.wg_budget or args.cols or args.lds_budget:
@@ -673,7 +705,7 @@ def main():
     # host-inclusive: the same steps with compact output rows (log-lik and
     # every parameter gradient, no dL/dP block: what a sampler consumes),
     # each followed by their D2H copy into pinned host memory
-    full_len = eng.outlen
+    full_len = 1 + B + 2 * C + 14 + 16 * C * B  # the full row (the dL/dP block included)
     eng.set_output(compact=True)
     d_out_c = torch.zeros((draws, eng.outlen), device=dev, dtype=torch.float64)
     h_out = torch.empty((draws, eng.outlen), dtype=torch.float64, pin_memory=True)
@@ -703,7 +735,7 @@ def main():
                           note="compact output rows (log-lik, branch / rate / mixture / frequency / "
                                "exchangeability gradients; no dL/dP block), each step followed by their D2H "
                                "copy into pinned host memory")
-    eng.set_output(compact=False)
+    eng.set_output(compact=args.compact)
 
     # cross-check: parameter set 0, draw 0 is the nominal point
     step(0)
@@ -831,10 +863,10 @@ def main():
             "limiter": "fp64 VALU issue / latency at two waves per SIMD: the SIMDs issue about half of the "
                        "wave-cycles and wait on s_waitcnt most of the rest (profiles/sq_counters.json); counted "
                        "HBM traffic is far below the 8 TB/s roof",
-            "hbm": {"achieved": achieved, "peak": PEAK_HBM_GBPS, "unit": "GB/s", "frac": achieved / PEAK_HBM_GBPS,
-                    "algorithmic_bytes_per_launch": alg,
-                    "survey_model_bytes_per_launch": survey_bytes(S, P_local, C, draws),
-                    "traffic_over_algorithmic": (traffic / alg) if traffic else None},
+            "hbm": dict({"achieved": achieved, "peak": PEAK_HBM_GBPS, "unit": "GB/s",
+                         "frac": achieved / PEAK_HBM_GBPS, "algorithmic_bytes_per_launch": alg,
+                         "survey_model_bytes_per_launch": survey_bytes(S, P_local, C, draws)},
+                        **counted_hbm(traffic, alg, kern_avg_ms)),
             "compute": compute,
         }
     else:
@@ -845,6 +877,7 @@ def main():
             "algorithmic_bytes_per_launch": alg,
             "survey_model_bytes_per_launch": survey_bytes(S, P_local, C, draws),
             "survey_flops_frac": achieved_tf / PEAK_FP64_TFLOPS,
+            "hbm": counted_hbm(traffic, alg, kern_avg_ms),
             "limiter": "latency / launch chain: one small dependent kernel per tree level (DESIGN.md 5b)",
         }
 
@@ -901,6 +934,7 @@ def main():
             "draws_100": draws_100,
             "program": info,
             "nominal_loglik": ll_nominal,
+            "row_doubles": eng.outlen,
             "kernel_source": kernel_source_hash(),
         }
         if args.multi_device:

@@ -8,6 +8,7 @@ there is no CPU fallback in the product path.
 """
 import ctypes
 import importlib.abc
+import importlib.machinery
 import importlib.util
 import os
 
@@ -51,13 +52,10 @@ SIGNATURES = {
     "phy_set_deep_stack": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
     "phy_deep_stack_in_lds": (ctypes.c_int, [ctypes.c_void_p]),
     "phy_set_recompute": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
-    "phy_set_graphs": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
     "phy_recomputed_partials": (ctypes.c_int, [ctypes.c_void_p]),
     "phy_set_engine": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
     "phy_set_output": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
     "phy_engine": (ctypes.c_int, [ctypes.c_void_p]),
-    "phy_set_flow": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
-    "phy_flow": (ctypes.c_int, [ctypes.c_void_p]),
     "phy_class_info": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_longlong), _c_int_p, _c_int_p,
                                       ctypes.POINTER(ctypes.c_longlong), ctypes.POINTER(ctypes.c_longlong),
                                       _c_int_p, _c_int_p]),
@@ -99,7 +97,9 @@ class _TorchAfterEngineGuard(importlib.abc.MetaPathFinder):
     only an actual import fails."""
 
     def find_spec(self, name, path=None, target=None):
-        if name == "torch" and _lib is not None:
+        # only a torch the other finders would actually import is guarded: in
+        # an environment without torch, probes still report it absent
+        if name == "torch" and _lib is not None and importlib.machinery.PathFinder.find_spec(name, path) is not None:
             return importlib.util.spec_from_loader(name, _GuardLoader())
         return None
 

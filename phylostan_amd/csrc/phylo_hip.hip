@@ -48,7 +48,7 @@
 #include <string>
 #include <vector>
 
-#include "phylo_hip.h"
+#include "phylo_hip_diag.h"
 
 namespace {
 
@@ -296,11 +296,6 @@ struct SweepArgs {
   // qfused (fin only): the Q-parameter chain rule (qgrad_kernel's work,
   // qgrad_body) runs after the finalize, in the same workgroup
   int qfused, kind;
-  // block-waves per category (sweep_kernel): a workgroup of C x wb waves runs
-  // wb pattern blocks side by side -- wave (bw, c) is a "virtual workgroup"
-  // of its own (scratch, deep entries, dL/dP and scalar slots), sharing the
-  // workgroup's LDS matrix records, staged once (wb > 1 needs a one-chunk plan)
-  int wb;
 };
 
 // LDS carve (16-B aligned pieces), K columns per lane:
@@ -318,9 +313,9 @@ __host__ __device__ inline size_t tip_lds_bytes(int S, int K) { return tip_nib_b
 __host__ __device__ inline size_t tail_doubles(int K, int ndl) {  // per wave
   return ndl > 0 ? (size_t)ndl * K * 2 * WAVE * 2 : (size_t)K * WAVE;
 }
-__host__ __device__ inline size_t lds_bytes(int S, int C, int R, int cap_m, int K, int ndl, int wb = 1) {
-  return tip_nib_bytes(S, K) * wb + 16 * 4 * sizeof(double) + (size_t)C * cap_m * R * 32 +
-         (size_t)C * wb * tail_doubles(K, ndl) * 8;
+__host__ __device__ inline size_t lds_bytes(int S, int C, int R, int cap_m, int K, int ndl) {
+  return tip_nib_bytes(S, K) + 16 * 4 * sizeof(double) + (size_t)C * cap_m * R * 32 +
+         (size_t)C * tail_doubles(K, ndl) * 8;
 }
 
 // Buffer resource over a workgroup's scratch / deep-stack region: loads past
@@ -688,23 +683,22 @@ __device__ void qgrad_body(const QgArgs& a, int draw, int tid, double* sh, const
 #ifndef PHY_WPE2
 #define PHY_WPE2 2  // waves per SIMD the K=2 kernel is register-budgeted for
 #endif
-template <int MAXT, int K, bool DL, int WB = 1>  // WB: block-waves per category (a.wb == WB)
+template <int MAXT, int K, bool DL>
 __global__ void __launch_bounds__(MAXT) __attribute__((amdgpu_waves_per_eu(MAXT <= 512 ? PHY_WPE2 : 4)))
     sweep_kernel(SweepArgs a, const int* __restrict__ prog) {
   extern __shared__ __attribute__((aligned(16))) unsigned char lds_raw[];
   const int lane = threadIdx.x & (WAVE - 1);
   const int C = a.C, nsteps = a.nsteps, nmat = a.nmat;
   const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int c = WB == 1 ? wv : wv % C, bw = WB == 1 ? 0 : wv / C;  // category, block-wave
+  const int c = wv;  // category
   const int nthreads = blockDim.x;
   const int draw = blockIdx.y;
-  // this wave's virtual workgroup: its own scratch / deep / slot regions
-  const int wg = (blockIdx.y * gridDim.x + blockIdx.x) * WB + bw;
+  const int wg = blockIdx.y * gridDim.x + blockIdx.x;
   const int rec = a.R * 4;  // doubles per matrix record
   const int ncolwg = C * WAVE;
 
-  unsigned char* tipl = lds_raw + (size_t)bw * tip_nib_bytes(a.S, K);  // this block-wave's tips
-  double* tvec = reinterpret_cast<double*>(lds_raw + tip_nib_bytes(a.S, K) * WB);  // [16][4]
+  unsigned char* tipl = lds_raw;  // the block's tips
+  double* tvec = reinterpret_cast<double*>(lds_raw + tip_nib_bytes(a.S, K));  // [16][4]
   double* mats0 = tvec + 64;
   if (threadIdx.x < 64) {  // published by the block loop's first barrier
     const unsigned b = threadIdx.x >> 2, j = threadIdx.x & 3;
@@ -783,26 +777,6 @@ __global__ void __launch_bounds__(MAXT) __attribute__((amdgpu_waves_per_eu(MAXT 
 
   // ---- this wave's chunk of matrix records in LDS (no barrier: private) ----
   int cur = -1, m0 = 0;
-  if constexpr (WB > 1) {  // one chunk holds every record; the category's block-waves stage it together, once
-    const double2* src = reinterpret_cast<const double2*>(pmat_c);
-    double2* dst = reinterpret_cast<double2*>(mats);
-    const int q2 = nmat * rec / 2;
-    for (int k0 = bw * WAVE + lane; k0 < q2; k0 += WB * WAVE * 8) {
-      double2 buf[8];
-#pragma unroll
-      for (int u = 0; u < 8; ++u) {
-        const int k = k0 + u * WB * WAVE;
-        buf[u] = (k < q2) ? src[k] : make_double2(0.0, 0.0);
-      }
-#pragma unroll
-      for (int u = 0; u < 8; ++u) {
-        const int k = k0 + u * WB * WAVE;
-        if (k < q2) dst[k] = buf[u];
-      }
-    }
-    WAIT_VMCNT0();
-    cur = 0;  // (published by the block loop's first barrier)
-  }
   auto ensure_chunk = [&](const Step& st) {
     const int ch = st.ch;
     if (ch == cur) return;  // wave-uniform
@@ -866,23 +840,18 @@ __global__ void __launch_bounds__(MAXT) __attribute__((amdgpu_waves_per_eu(MAXT 
     }
   };
 
-  // blocks: this wave's virtual workgroup takes blocks vg, vg + VG, ... (vg its
-  // index inside the draw, VG = gridDim.x * WB of them); every wave runs the
-  // same number of trips (the workgroup's barriers), a trip past the last
-  // block is a pass without work (the launch keeps VG <= nblk, so every
-  // virtual workgroup has at least one real block and writes its slots)
-  const int VG = gridDim.x * WB, vg = blockIdx.x * WB + bw;
-  // (one block-wave: the workgroup's own blocks, every trip real)
-  const int trips = WB == 1 ? (a.nblk - vg + VG - 1) / VG : (a.nblk + VG - 1) / VG;
+  // blocks: the workgroup takes blocks blockIdx.x, + gridDim.x, ... of its
+  // draw (the launch keeps gridDim.x <= nblk: every workgroup has a block)
+  const int VG = gridDim.x, vg = blockIdx.x;
+  const int trips = (a.nblk - vg + VG - 1) / VG;
   for (int trip = 0; trip < trips; ++trip) {
     const int blk = vg + trip * VG;
-    const bool real = WB == 1 || blk < a.nblk;  // wave-uniform
 #pragma unroll
     for (int k = 0; k < K; ++k) lofs[k] = (blk * WAVE * K + k * WAVE + lane < a.P) ? lcol[k] : OOB;
     __syncthreads();  // the previous block's tip / root-exchange reads are done
     // stage this block's tip bytes in LDS: S rows x 64K bytes, shared by the
-    // C category-waves of the block-wave and by both passes (8 loads in flight per thread)
-    if (real) {
+    // C category-waves and by both passes (8 loads in flight per thread)
+    {
       const uint32_t* src = reinterpret_cast<const uint32_t*>(a.tips);
       uint32_t* dst = reinterpret_cast<uint32_t*>(tipl);
       const int rowq = a.Ppad / 8;
@@ -980,7 +949,7 @@ __global__ void __launch_bounds__(MAXT) __attribute__((amdgpu_waves_per_eu(MAXT 
         for (int k = 0; k < K; ++k) proot[k] = pv[k];                                                                 \
       }                                                                                                               \
     } while (0)
-    if (real) {
+    {
       V4 dA[K], dB[K];
 #pragma unroll
       for (int k = 0; k < K; ++k) dA[k] = {0.0, 0.0, 0.0, 0.0};  // step 0 has no internal child
@@ -994,7 +963,7 @@ __global__ void __launch_bounds__(MAXT) __attribute__((amdgpu_waves_per_eu(MAXT 
     }
 
     // ------------------------- root / site log L -------------------------
-    // (the C category waves of this block-wave exchange through their tails)
+    // (the C category waves exchange through their tails)
     double fp[K];
 #pragma unroll
     for (int k = 0; k < K; ++k) {
@@ -1006,10 +975,9 @@ __global__ void __launch_bounds__(MAXT) __attribute__((amdgpu_waves_per_eu(MAXT 
 #pragma unroll
     for (int k = 0; k < K; ++k) {
       L[k] = 0.0;
-      for (int cc = 0; cc < C; ++cc) L[k] += tail0[(size_t)(bw * C + cc) * tstride + k * WAVE + lane];
+      for (int cc = 0; cc < C; ++cc) L[k] += tail0[(size_t)cc * tstride + k * WAVE + lane];
     }
     __syncthreads();  // every wave has read the exchange before deep entries are rewritten
-    if (!real) continue;  // (a trip without a block: no columns, no reverse)
     V4 topr[K];
 #pragma unroll
     for (int k = 0; k < K; ++k) {
@@ -1237,12 +1205,11 @@ __global__ void __launch_bounds__(MAXT) __attribute__((amdgpu_waves_per_eu(MAXT 
     // a release fence here would write back the whole L2 per workgroup.
     WAIT_VMCNT0();
     // fin: the finalize runs here; its LDS (inner products [C][B], then the
-    // waves' scalar partials [WB][C][8], then qgrad's) reuses the sweep's,
-    // once every wave is done.  With WB block-waves the category's dL/dP is
-    // the sum of their WB slots, in block-wave order (read after the barrier)
+    // waves' scalar partials [C][8], then qgrad's) reuses the sweep's, once
+    // every wave is done
     double* innerL = mats0;
     double* scalL = mats0 + (size_t)C * a.B;
-    if (a.fin || WB > 1) __syncthreads();
+    if (a.fin) __syncthreads();
     const double* Qd = a.eig + (size_t)draw * EIG_LEN + EIG_Q;
     double* gout = a.grows + (size_t)draw * a.grows_stride;
     double* inner_d = a.inner + (size_t)draw * C * a.B;
@@ -1252,19 +1219,15 @@ __global__ void __launch_bounds__(MAXT) __attribute__((amdgpu_waves_per_eu(MAXT 
     const double q0 = Qd[j * 4 + 0], q1 = Qd[j * 4 + 1], q2 = Qd[j * 4 + 2], q3 = Qd[j * 4 + 3];
     const int tot = nmat * 16;  // a multiple of 16: 16-lane groups are whole
     constexpr int U = PHY_EPI_U;
-    const size_t vstride = (size_t)C * nmat * 16;            // one virtual workgroup's slots
-    const double* gs0 = gs - (size_t)bw * vstride;           // block-wave 0's slot of category c
-    for (int k0 = bw * WAVE + lane; k0 < tot; k0 += WB * WAVE * U) {
+    for (int k0 = lane; k0 < tot; k0 += WAVE * U) {
       double g[U], qp[U];
       int bb[U];
 #pragma unroll
       for (int u = 0; u < U; ++u) {  // all loads in flight before any use
-        const int k = k0 + u * WB * WAVE;
+        const int k = k0 + u * WAVE;
         const int kc = k < tot ? k : lane;
         const int mm = kc >> 4;
-        g[u] = __hip_atomic_load(gs0 + kc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        for (int v = 1; v < WB; ++v)
-          g[u] += __hip_atomic_load(gs0 + v * vstride + kc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        g[u] = __hip_atomic_load(gs + kc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         const double2* col = reinterpret_cast<const double2*>(pmat_c + (size_t)mm * rec + kk * 4);  // column kk of P
         const double2 c01 = col[0], c23 = col[1];
         qp[u] = fma(q3, c23.y, fma(q2, c23.x, fma(q1, c01.y, q0 * c01.x)));
@@ -1272,7 +1235,7 @@ __global__ void __launch_bounds__(MAXT) __attribute__((amdgpu_waves_per_eu(MAXT 
       }
 #pragma unroll
       for (int u = 0; u < U; ++u) {
-        const int k = k0 + u * WB * WAVE;
+        const int k = k0 + u * WAVE;
         if (k < tot) {
           double sv = g[u] * qp[u];
           sv += __shfl_xor(sv, 8, 16);
@@ -1314,11 +1277,7 @@ __global__ void __launch_bounds__(MAXT) __attribute__((amdgpu_waves_per_eu(MAXT 
         out[1 + B + cc] = sacc;
       }
       if (threadIdx.x == 0) {
-        auto tot8 = [&](int cc, int jj) {  // over the block-waves in order
-          double t = scalL[(size_t)cc * 8 + jj];
-          for (int v = 1; v < WB; ++v) t += scalL[(size_t)(v * C + cc) * 8 + jj];
-          return t;
-        };
+        auto tot8 = [&](int cc, int jj) { return scalL[(size_t)cc * 8 + jj]; };
         const double ll = tot8(0, 0);
         out[0] = isfinite(ll) ? ll : -INFINITY;
         for (int cc = 0; cc < C; ++cc) out[1 + B + C + cc] = tot8(cc, 1);
@@ -1329,7 +1288,7 @@ __global__ void __launch_bounds__(MAXT) __attribute__((amdgpu_waves_per_eu(MAXT 
         }
       }
       if (a.qfused) {  // the Q-parameter chain rule (qgrad_kernel's work, same bits)
-        double* qsh = scalL + (size_t)C * 8 * WB;
+        double* qsh = scalL + (size_t)C * 8;
         const QgArgs q{a.eig, a.model, a.blens, a.grows, a.grows_stride, a.out, a.outlen, C, B, a.kind};
         __syncthreads();  // dL/dP rows and the root term visible to the workgroup
         qgrad_body(q, draw, threadIdx.x, qsh);
@@ -2211,12 +2170,7 @@ struct phy_ctx {
   int wg_budget, cols_pref, wg_cap, lds_budget;
   int cu_count = 256, wg_resident = 512;  // resident workgroups of the current plan
   int K = 1;                   // columns per lane of the current plan
-  int wb = 1;                  // block-waves per category of the current plan (sweep_kernel's wb)
-  bool wb_pref = false;        // PHY_WB=1: two block-waves per category when one chunk fits (opt-in, slower)
   bool klat = false;           // K = 1 latency plan (sweep_kernel<512, 1, .>: no register spills)
-  bool klat_pref = true;       // PHY_KLAT=0: the latency plan keeps the four-wave K = 1 kernel
-  bool eig_fuse_pref = true;   // PHY_EIG_FUSE=0: small device batches take eig_kernel + pmat_kernel<false>
-  int eig_fuse_max = EIG_FUSE_MAX;  // PHY_EIG_FUSE_MAX: draws per launch up to which pmat_kernel forms them
   // the quad sweep (quad_engine.inc) for calls of <= QUAD_MAX_DRAWS draws
   bool quad_pref = true;       // PHY_QUAD=0: off
   // the multi-wave quad sweep (qmw_kernel): W waves per category share a block
@@ -2246,12 +2200,6 @@ struct phy_ctx {
   // engine_pref 0 = automatic, 1 = pattern, 2 = class
   int engine = 0, engine_pref = 0;
   ClassEngine* ce = nullptr;
-  // the class sweep as one dataflow launch (cls_flow_kernel) instead of level
-  // launches: opt-in (PHY_FLOW=1 / phy_set_flow(ctx, 1)); never for the
-  // shards of a same-device multi context (their launches run concurrently,
-  // and the flow grid must be resident); flow_wgs = its resident grid
-  bool flow_pref = true, flow_ok = true;
-  int flow_wgs[2] = {0, 0};  // [root has a tip child]: that variant's resident grid
   MultiState* ms = nullptr;  // a multi-device context (phy_create_multi): its shards do the work
   int compact = 0;             // output rows without the dL/dP block (phy_set_output)
   double* d_grows = nullptr;   // dL/dP rows when compact: [max_draws][16 C B]
@@ -2260,6 +2208,9 @@ struct phy_ctx {
   std::vector<int32_t> h_peel;
   std::vector<int> vec_of, gpos;
   hipStream_t stream;
+  // phy_eval_device on the legacy null stream: the context's stream waits for
+  // the null stream's work (nin), the null stream for the evaluation (nout)
+  hipEvent_t ev_nin = nullptr, ev_nout = nullptr;
   std::vector<int> prog;  // host copy of the program (chunk fields per plan)
   uint8_t* d_tips = nullptr;
   double* d_w = nullptr;
@@ -2282,9 +2233,6 @@ struct phy_ctx {
   double* h_out = nullptr;  // pinned [PIN_DRAWS][full output row]
   // the small path's kernel-side views of h_in / h_out when the kernels read
   // their operands from / write their rows to pinned host memory directly
-  // (PHY_DIRECT_IN / PHY_DIRECT_OUT), else nullptr: blits through d_in / d_out
-  const double* h_in_dev = nullptr;
-  double* h_out_dev = nullptr;
   double* d_in = nullptr;   // device [PIN_DRAWS][B + model_len + EIG_LEN]
   int pending = 0;          // draws of a phy_eval_submit not yet collected by phy_eval_wait
   double2* d_scratch = nullptr;
@@ -2292,19 +2240,6 @@ struct phy_ctx {
   double* d_gslot = nullptr;
   double* d_sslot = nullptr;
   bool timing = false;
-  // HIP graphs of whole evaluations (launch_graphed): one per operand set,
-  // replayed while plan_gen (bumped by every plan / buffer / engine change)
-  // is unchanged; PHY_GRAPH=0 turns them off
-  struct Graph {
-    int n;
-    const void *bl, *md, *out, *site, *st;
-    long gen;
-    hipGraphExec_t ex;
-  };
-  std::vector<Graph> graphs;
-  Graph seen{};                // the last operand set run directly: captured when it comes again
-  long plan_gen = 0;
-  bool graph_pref = false;     // measured no gain: opt-in
   std::vector<hipEvent_t> ev;  // pairs
   int ev_used = 0;
   double timed_ms = 0.0;
@@ -2327,7 +2262,8 @@ void free_ctx(phy_ctx* c) {
   if (c->h_in) (void)hipHostFree(c->h_in);
   if (c->h_out) (void)hipHostFree(c->h_out);
   for (hipEvent_t e : c->ev) (void)hipEventDestroy(e);
-  for (auto& g : c->graphs) (void)hipGraphExecDestroy(g.ex);
+  if (c->ev_nin) (void)hipEventDestroy(c->ev_nin);
+  if (c->ev_nout) (void)hipEventDestroy(c->ev_nout);
   free_class_engine(c->ce);
   free_multi(c->ms);
   if (c->stream) (void)hipStreamDestroy(c->stream);
@@ -2528,12 +2464,6 @@ constexpr size_t LDS_CAP = 160 * 1024;
 
 constexpr int PIN_DRAWS = 128;  // phy_eval batches up to this size go through pinned staging
                                 // (ADVI's elbo_samples = 100 fits: phylostan.py:47)
-#ifndef PHY_DIRECT_OUT_DEFAULT
-#define PHY_DIRECT_OUT_DEFAULT 0
-#endif
-#ifndef PHY_DIRECT_IN_DEFAULT
-#define PHY_DIRECT_IN_DEFAULT 0
-#endif
 bool env_flag(const char* name, int dflt) {
   const char* v = getenv(name);
   return v ? atoi(v) != 0 : dflt != 0;
@@ -2546,8 +2476,7 @@ int nblk_for(int P, int K) { return (P + WAVE * K - 1) / (WAVE * K); }
 // workgroups, 128 VGPRs: spills) for wide launches with C > 8, and the
 // sampler's latency plan (a few draws: at most one wave per SIMD is busy)
 // at 256 VGPRs without spills (lat).
-const void* sweep_kernel_ptr(int K, bool dl, bool lat, int wb = 1) {
-  if (K == 2 && wb == 2) return (const void*)sweep_kernel<512, 2, true, 2>;  // (the block-wave plan keeps the deep stack in LDS)
+const void* sweep_kernel_ptr(int K, bool dl, bool lat) {
   if (K == 2) return dl ? (const void*)sweep_kernel<512, 2, true> : (const void*)sweep_kernel<512, 2, false>;
   if (lat) return dl ? (const void*)sweep_kernel<512, 1, true> : (const void*)sweep_kernel<512, 1, false>;
   return dl ? (const void*)sweep_kernel<1024, 1, true> : (const void*)sweep_kernel<1024, 1, false>;
@@ -2573,7 +2502,7 @@ int plan_chunks(phy_ctx* c) {
     K = c->C <= 8 ? 2 : 1;
     if (K == 2 && (long)c->max_draws * nblk_for(c->P, 1) * c->C <= 4L * c->cu_count) {
       K = 1;
-      lat = c->klat_pref;
+      lat = true;
     }
   }
   if (K == 2 && c->C > 8) return fail(PHY_EINVAL, "two columns per lane need C <= 8");
@@ -2618,33 +2547,17 @@ int plan_chunks(phy_ctx* c) {
     for (int t = by_waves; t >= 1; --t)
       if (place(LDS_CAP / t, t == 1)) break;
   }
-  // Block-waves (the batched two-column plan): a workgroup of C x wb waves --
-  // wb pattern blocks side by side, two waves per SIMD as before -- whose LDS
-  // holds EVERY matrix record of the draw (one chunk, staged once per
-  // workgroup instead of once per chunk per block) and the whole deep stack;
-  // taken when it fits one workgroup per CU (fluA: 2 x 4 waves, 159 KB)
-  int wb = 1;
-  if (K == 2 && !lat && c->wb_pref && c->lds_budget == 0 && c->deep_pref != 2 && c->C <= 4) {
-    const int w = std::min(2, nb);  // (sweep_kernel's WB instantiations: 1, 2)
-    if (w >= 2 && lds_bytes(c->S, c->C, c->R, c->nmat, K, c->ndeep, w) <= LDS_CAP) {
-      wb = w;
-      cap = c->nmat;
-      ndl = c->ndeep;
-    }
-  }
-  const size_t lds = lds_bytes(c->S, c->C, c->R, cap, K, ndl, wb);
+  const size_t lds = lds_bytes(c->S, c->C, c->R, cap, K, ndl);
   if (lds > LDS_CAP) return fail(PHY_EINVAL, "tree too large for LDS (tips of one block)");
   c->K = K;
-  c->wb = wb;
   c->klat = lat;
   c->nblk = nb;
-  ++c->plan_gen;
-  c->wg_resident = wb > 1 ? c->cu_count : c->cu_count * std::min<int>(by_waves, (int)(LDS_CAP / lds));
+  c->wg_resident = c->cu_count * std::min<int>(by_waves, (int)(LDS_CAP / lds));
   {
     // workgroup regions the largest launch of this plan may use
     // (launch_pattern's gx per draw), grown here so no launch fails
     const long budget = c->wg_budget > 0 ? c->wg_budget : c->wg_resident;
-    const long need = std::min<long>((long)c->max_draws * nb, (budget + c->max_draws) * wb);  // virtual workgroups
+    const long need = std::min<long>((long)c->max_draws * nb, budget + c->max_draws);
     if (need > c->wg_cap) {
       HIP_TRY(hipStreamSynchronize(c->stream));
       int rc = alloc_wg_buffers(c, need);
@@ -2730,7 +2643,6 @@ int ensure_class_plan(phy_ctx* c) {
 }
 
 int select_engine(phy_ctx* c) {
-  ++c->plan_gen;
   c->engine = 0;
   if (c->engine_pref == 1) return PHY_OK;
   if (c->engine_pref == 0 && c->P < 16384) return PHY_OK;
@@ -2744,14 +2656,6 @@ int select_engine(phy_ctx* c) {
     c->ce = nullptr;
   }
   return PHY_OK;
-}
-
-// The class sweep runs as the dataflow launch (cls_flow_kernel) when it is
-// preferred and allowed and the categories fit its workgroup (C waves <= 16).
-// (a plan with a top chain has no dataflow items: build with PHY_CHAIN=0 for it)
-bool flow_applies(const phy_ctx* ctx) {
-  return ctx->flow_pref && ctx->flow_ok && ctx->C <= 16 && ctx->flow_wgs[0] > 0 && ctx->flow_wgs[1] > 0 &&
-         !(ctx->ce && ctx->ce->chain_m > 0);
 }
 
 // HIP events around the timed part of one launch (phy_timing_start)
@@ -2789,47 +2693,15 @@ int launch_class(phy_ctx* ctx, int n, const double* d_blens, const double* d_mod
   ClassArgs a = class_args(e, ctx->d_pmat, d_model, ctx->extra);
   const int dcn = n * C;
   hipEvent_t e0 = nullptr, e1 = nullptr;
-  const bool flow = flow_applies(ctx);
-  if (flow) {  // counters zeroed on this stream, then the whole sweep as one dataflow launch
-    HIP_TRY(hipMemsetAsync(e->d_fcnt, 0, (4 + (size_t)n * e->ncnt) * sizeof(unsigned), st));
-  }
   if (ctx->timing && (rc = timing_begin(ctx, st, &e0, &e1))) return rc;
-  if (flow) {
-    unsigned long long* trace = nullptr;
-    const char* tpath = getenv("PHY_FLOW_TRACE");  // diagnostics: per-item wall-clock trace appended to this file
-    if (tpath && *tpath) HIP_TRY(hipMallocAsync((void**)&trace, sizeof(unsigned long long) * 4 * e->nitems * n, st));
-    const FlowArgs fa{e->d_items, e->nitems, n, e->d_fcnt + 4, e->ncnt, e->d_fcnt, trace};
-    const long long total = (long long)e->nitems * n;
-    if (total >= (1ll << 31)) return fail(PHY_ERANGE, "class sweep: too many dataflow items x draws");
-    const int grid = (int)std::min<long long>(total, (long long)ctx->flow_wgs[e->root_tips ? 1 : 0]);
-    auto fk = C <= 4 ? (e->root_tips ? cls_flow_kernel<256, true> : cls_flow_kernel<256, false>)
-                     : (e->root_tips ? cls_flow_kernel<1024, true> : cls_flow_kernel<1024, false>);
-    hipLaunchKernelGGL(fk, dim3(std::max(grid, 1)), dim3(C * WAVE), 0, st, a, fa);
-    if (trace) {  // items (kind, idx, level-free), then the trace rows; one record per launch
-      const size_t nt = (size_t)4 * e->nitems * n;
-      std::vector<unsigned long long> h(nt);
-      std::vector<FItem> hi(e->nitems);
-      HIP_TRY(hipMemcpyAsync(h.data(), trace, nt * sizeof(unsigned long long), hipMemcpyDeviceToHost, st));
-      HIP_TRY(hipMemcpyAsync(hi.data(), e->d_items, hi.size() * sizeof(FItem), hipMemcpyDeviceToHost, st));
-      HIP_TRY(hipStreamSynchronize(st));
-      HIP_TRY(hipFree(trace));
-      if (FILE* fp = fopen(tpath, "ab")) {
-        const int hdr[4] = {e->nitems, n, grid, (int)sizeof(FItem)};
-        fwrite(hdr, sizeof(int), 4, fp);
-        fwrite(hi.data(), sizeof(FItem), hi.size(), fp);
-        fwrite(h.data(), sizeof(unsigned long long), nt, fp);
-        fclose(fp);
-      }
-    }
-  }
-  if (!flow && e->Lc > 0)  // levels 1..Lc: one workgroup per (bottom clade, dc)
+  if (e->Lc > 0)  // levels 1..Lc: one workgroup per (bottom clade, dc)
     hipLaunchKernelGGL(cls_clade_fwd_kernel, dim3(e->nclade, dcn), dim3(CLADE_THREADS), 0, st, a,
                        (const CladeLevel*)e->d_clade, e->Lc);
-  const bool chain = !flow && e->chain_m > 0;
+  const bool chain = e->chain_m > 0;
   const ChainArgs ca{e->d_link, e->d_ctab, e->d_crep, e->chain_m, e->chain_ntop, e->chain_ntp, e->chain_toff};
   const int chain_wgs = (e->chain_ntp / WAVE + CLS_WPG - 1) / CLS_WPG;
   auto in_chain = [&](int l) { return chain && l >= e->chain_lo && l <= e->chain_hi; };
-  for (int l = e->Lc + 1; l < e->levels && !flow; ++l) {
+  for (int l = e->Lc + 1; l < e->levels; ++l) {
     const ClassLevel& L = e->lv[l];
     if (!L.nchunk || in_chain(l) || L.pair == 2) continue;
     a.first = L.chunk0;
@@ -2849,19 +2721,17 @@ int launch_class(phy_ctx* ctx, int n, const double* d_blens, const double* d_mod
     hipLaunchKernelGGL(e->chain_m <= 4 ? cls_chain_fwd_kernel<4> : e->chain_m == 5 ? cls_chain_fwd_kernel<5>
                        : e->chain_m <= 6 ? cls_chain_fwd_kernel<6> : cls_chain_fwd_kernel<CHAIN_MAX>,
                        dim3(chain_wgs, dcn), dim3(CLS_THREADS), 0, st, a, ca);
-  if (!flow) {
-    auto rk = C <= 4 ? (e->root_tips ? cls_root_kernel<256, true> : cls_root_kernel<256, false>)
-                     : (e->root_tips ? cls_root_kernel<1024, true> : cls_root_kernel<1024, false>);
-    if (root_chain) {
-      const int m = e->chain_m;
-      rk = e->root_tips ? (m <= 4 ? cls_root_kernel<256, true, 4> : m == 5 ? cls_root_kernel<256, true, 5>
-                           : m <= 6 ? cls_root_kernel<256, true, 6> : cls_root_kernel<256, true, CHAIN_MAX>)
-                        : (m <= 4 ? cls_root_kernel<256, false, 4> : m == 5 ? cls_root_kernel<256, false, 5>
-                           : m <= 6 ? cls_root_kernel<256, false, 6> : cls_root_kernel<256, false, CHAIN_MAX>);
-    }
-    hipLaunchKernelGGL(rk, dim3(e->nrootch, n), dim3(C * WAVE), 0, st, a, ca);
+  auto rk = C <= 4 ? (e->root_tips ? cls_root_kernel<256, true> : cls_root_kernel<256, false>)
+                   : (e->root_tips ? cls_root_kernel<1024, true> : cls_root_kernel<1024, false>);
+  if (root_chain) {
+    const int m = e->chain_m;
+    rk = e->root_tips ? (m <= 4 ? cls_root_kernel<256, true, 4> : m == 5 ? cls_root_kernel<256, true, 5>
+                         : m <= 6 ? cls_root_kernel<256, true, 6> : cls_root_kernel<256, true, CHAIN_MAX>)
+                      : (m <= 4 ? cls_root_kernel<256, false, 4> : m == 5 ? cls_root_kernel<256, false, 5>
+                         : m <= 6 ? cls_root_kernel<256, false, 6> : cls_root_kernel<256, false, CHAIN_MAX>);
   }
-  for (int l = e->levels - 1; l > e->Lc && !flow; --l) {
+  hipLaunchKernelGGL(rk, dim3(e->nrootch, n), dim3(C * WAVE), 0, st, a, ca);
+  for (int l = e->levels - 1; l > e->Lc; --l) {
     const ClassLevel& L = e->lv[l];
     if (L.ntile) {
       a.first = L.tile0;
@@ -2889,7 +2759,7 @@ int launch_class(phy_ctx* ctx, int n, const double* d_blens, const double* d_mod
         hipLaunchKernelGGL(cls_rev_kernel, dim3((L.nchunk + CLS_WPG - 1) / CLS_WPG, dcn), dim3(CLS_THREADS), 0, st, a);
     }
   }
-  if (!flow && e->Lc > 0) {
+  if (e->Lc > 0) {
     if (e->nrtile)
       hipLaunchKernelGGL(cls_red_list_kernel, dim3((e->nrtile + CLS_WPG - 1) / CLS_WPG, dcn), dim3(CLS_THREADS), 0, st, a,
                          (const int*)e->d_rtile, e->nrtile);
@@ -2908,8 +2778,7 @@ int launch_class(phy_ctx* ctx, int n, const double* d_blens, const double* d_mod
   const size_t ncb = (size_t)n * C * B;
   EpiArgs ea{e->d_gpart, e->d_gbase, e->d_gcount, e->d_sslot, ctx->d_pmat, ctx->eig_cur, d_blens, d_model,
              ctx->d_gpos, grows, gstride, d_out, epi, epi + ncb, epi + 17 * ncb,
-             e->d_epicnt, C, B, ctx->nmat, ctx->R, std::max(e->ngs, 1), e->nrootch, phy_output_len(ctx), ctx->kind,
-             flow ? e->d_fcnt : nullptr};
+             e->d_epicnt, C, B, ctx->nmat, ctx->R, std::max(e->ngs, 1), e->nrootch, phy_output_len(ctx), ctx->kind};
   hipLaunchKernelGGL(cls_epi_kernel, dim3(C * B, n), dim3(EPI_THREADS), 0, st, ea);
   *qdone = true;
   HIP_TRY(hipGetLastError());
@@ -2947,7 +2816,7 @@ int launch(phy_ctx* ctx, int n, const double* d_blens, const double* d_model, do
     // eigensystems: given (host-formed, the small host-buffer path); small
     // device batches: each pmat wave forms its draw's (one launch less);
     // large ones: one thread per draw first
-    const int with_eig = (!d_eig_in && n <= ctx->eig_fuse_max && ctx->eig_fuse_pref) ? 1 : 0;
+    const int with_eig = (!d_eig_in && n <= EIG_FUSE_MAX) ? 1 : 0;
     PmatArgs pa{d_model, d_blens, ctx->d_mat_branch, const_cast<double*>(ctx->eig_cur), ctx->d_pmat, C, B, ctx->kind,
                 ctx->nmat, n, ctx->R, ctx->extra, with_eig};
     if (!with_eig && !d_eig_in) {
@@ -2980,76 +2849,6 @@ int launch(phy_ctx* ctx, int n, const double* d_blens, const double* d_model, do
   return PHY_OK;
 }
 
-// One evaluation's stream work (`body`: launch(), with the small path's
-// copies around it) through a HIP graph (opt-in: phy_set_graphs; measured
-// on MI355X, a 4-draw fluA call 167 -> 174 us, the synthetic shard-8
-// projection 3251 -> 3273 evals/s -- the class sweep is bound by the
-// GPU-side gaps between its dependent kernels, which a graph keeps, not by
-// host launch cost): the first run of an operand set
-// (draw count, buffers, stream) is direct -- it makes any lazy allocation
-// (class reserves) -- the second is captured and instantiated,
-// later ones replay it: one graph launch instead of up to ~50 kernel
-// launches (the class sweep's levels).  Engine reserves are grown before
-// the lookup; growth or any replan bumps plan_gen, and stale graphs are
-// rebuilt.  Timed evaluations (phy_timing_*) and a failed capture run
-// direct.
-template <typename F>
-int launch_graphed(phy_ctx* ctx, int n, const void* bl, const void* md, const void* out, const void* site,
-                   hipStream_t st, F&& body) {
-  if (!ctx->graph_pref || ctx->timing) return body();
-  {
-    int rc = PHY_OK;
-    if (ctx->engine == 1 && n > ctx->ce->max_draws) {
-      if ((rc = class_engine_reserve(ctx->ce, n, st))) return rc;
-      ++ctx->plan_gen;
-    }
-  }
-  const phy_ctx::Graph key{n, bl, md, out, site, (const void*)st, ctx->plan_gen, nullptr};
-  auto same = [&](const phy_ctx::Graph& g) {
-    return g.n == key.n && g.bl == key.bl && g.md == key.md && g.out == key.out && g.site == key.site &&
-           g.st == key.st && g.gen == key.gen;
-  };
-  for (auto& g : ctx->graphs)
-    if (same(g)) {
-      HIP_TRY(hipGraphLaunch(g.ex, st));
-      return PHY_OK;
-    }
-  if (!same(ctx->seen)) {  // first sighting: direct
-    ctx->seen = key;
-    return body();
-  }
-  // stale entries (older plans) go first, then the oldest beyond 8
-  for (size_t i = 0; i < ctx->graphs.size();)
-    if (ctx->graphs[i].gen != ctx->plan_gen) {
-      (void)hipGraphExecDestroy(ctx->graphs[i].ex);
-      ctx->graphs.erase(ctx->graphs.begin() + i);
-    } else {
-      ++i;
-    }
-  if (ctx->graphs.size() >= 8) {
-    (void)hipGraphExecDestroy(ctx->graphs.front().ex);
-    ctx->graphs.erase(ctx->graphs.begin());
-  }
-  HIP_TRY(hipStreamBeginCapture(st, hipStreamCaptureModeThreadLocal));
-  const int rc = body();
-  hipGraph_t g = nullptr;
-  const hipError_t ec = hipStreamEndCapture(st, &g);
-  hipGraphExec_t ex = nullptr;
-  hipError_t ei = hipErrorUnknown;
-  if (rc == PHY_OK && ec == hipSuccess && g) ei = hipGraphInstantiate(&ex, g, nullptr, nullptr, 0);
-  if (g) (void)hipGraphDestroy(g);
-  if (rc != PHY_OK || ec != hipSuccess || ei != hipSuccess) {  // run it direct, and stop capturing
-    (void)hipGetLastError();
-    ctx->graph_pref = false;
-    return body();
-  }
-  phy_ctx::Graph ent = key;
-  ent.ex = ex;
-  ctx->graphs.push_back(ent);
-  HIP_TRY(hipGraphLaunch(ex, st));
-  return PHY_OK;
-}
-
 // The quad sweep (quad_engine.inc) for a small call: one workgroup of C
 // waves per 16-column block and draw, as many blocks per workgroup as keep
 // the launch within one wave per SIMD; then the pattern sweep's epilogue
@@ -3075,7 +2874,6 @@ int launch_quad(phy_ctx* ctx, int n, const double* d_blens, const double* d_mode
       if (rc) return rc;
       ctx->qscr_wgs = wgs;
     }
-    ++ctx->plan_gen;
   }
   // the split epilogue (qfin_kernel): items of bper branches x C categories per workgroup
   const int bper = std::max(1, std::min((B + 15) / 16, QFIN_ITEMS / C));
@@ -3087,14 +2885,13 @@ int launch_quad(phy_ctx* ctx, int n, const double* d_blens, const double* d_mode
     if (rc) return rc;
     HIP_TRY(hipMemset(ctx->d_qfcnt, 0, (size_t)QUAD_MAX_DRAWS * sizeof(unsigned long long)));
     HIP_TRY(hipDeviceSynchronize());
-    ++ctx->plan_gen;
   }
   QuadArgs qa;
   qa.s = SweepArgs{ctx->d_tips,  ctx->d_w,     ctx->d_pmat,  d_model,      ctx->d_scratch, ctx->d_dstk,
                    ctx->d_gslot, ctx->d_sslot, d_site,       d_out,        ctx->d_mat_branch, ctx->eig_cur,
                    ctx->d_inner, ctx->S,       ctx->P,       ctx->Ppad,    C,              ctx->nsteps,
                    ctx->nslots,  ctx->ndeep,   0,            ctx->nblk,    ctx->nmat,    ctx->R,         ctx->nmat,
-                   B,            phy_output_len(ctx), 0, ctx->extra, 0, d_blens, grows, gstride, 0, ctx->kind, 1};
+                   B,            phy_output_len(ctx), 0, ctx->extra, 0, d_blens, grows, gstride, 0, ctx->kind};
   qa.qscr = ctx->d_qscr;
   qa.nblk = nb;
   qa.pmat_out = ctx->d_pmat;
@@ -3149,31 +2946,29 @@ int launch_pattern(phy_ctx* ctx, int n, const double* d_blens, const double* d_m
     return launch_quad(ctx, n, d_blens, d_model, d_out, d_site, st, grows, gstride, qdone);
   // persistent workgroups: the explicit budget, else exactly what is resident
   const int budget = ctx->wg_budget > 0 ? ctx->wg_budget : ctx->wg_resident;
-  // block-waves of this launch: at most one per block, so every virtual
-  // workgroup (gx x wb of them per draw, <= nblk) has a block to write its slots
-  const int wb = std::max(1, std::min(ctx->wb, ctx->nblk));
-  const int gx = std::max(1, std::min(ctx->nblk / wb, (budget + n - 1) / n));
-  if ((size_t)gx * wb * n > (size_t)ctx->wg_cap) return fail(PHY_ERANGE, "workgroup cap exceeded");
-  const size_t lds = lds_bytes(ctx->S, C, ctx->R, ctx->cap_m, ctx->K, ctx->ndl, wb);
+  // (at most one workgroup per block, so every workgroup has a block to write its slots)
+  const int gx = std::max(1, std::min(ctx->nblk, (budget + n - 1) / n));
+  if ((size_t)gx * n > (size_t)ctx->wg_cap) return fail(PHY_ERANGE, "workgroup cap exceeded");
+  const size_t lds = lds_bytes(ctx->S, C, ctx->R, ctx->cap_m, ctx->K, ctx->ndl);
   const int g_direct = (gx == 1) ? 1 : 0;
-  // finalize inside the sweep when its LDS holds [C][B] + [wb][C][8] doubles
+  // finalize inside the sweep when its LDS holds [C][B] + [C][8] doubles
   // past the tips; the chain rule too when QG_SHARED more fit
-  const size_t room = lds - tip_nib_bytes(ctx->S, ctx->K) * wb - 16 * 4 * sizeof(double);
-  const int fin = (g_direct && ctx->fin_pref && ((size_t)C * B + 8 * C * wb) * 8 <= room) ? 1 : 0;
-  const int qf = (fin && ctx->qfuse_pref && ((size_t)C * B + 8 * C * wb + QG_SHARED) * 8 <= room) ? 1 : 0;
+  const size_t room = lds - tip_nib_bytes(ctx->S, ctx->K) - 16 * 4 * sizeof(double);
+  const int fin = (g_direct && ctx->fin_pref && ((size_t)C * B + 8 * C) * 8 <= room) ? 1 : 0;
+  const int qf = (fin && ctx->qfuse_pref && ((size_t)C * B + 8 * C + QG_SHARED) * 8 <= room) ? 1 : 0;
   SweepArgs sa{ctx->d_tips,  ctx->d_w,     ctx->d_pmat,  d_model,      ctx->d_scratch, ctx->d_dstk,
                ctx->d_gslot, ctx->d_sslot, d_site,       d_out,        ctx->d_mat_branch, ctx->eig_cur,
                ctx->d_inner, ctx->S,       ctx->P,       ctx->Ppad,    C,              ctx->nsteps,
                ctx->nslots,  ctx->ndeep,   ctx->ndl,     ctx->nblk,    ctx->nmat,    ctx->R,         ctx->cap_m,
                B,            phy_output_len(ctx), g_direct, ctx->extra, fin, d_blens, grows, gstride,
-               qf,           ctx->kind,      wb};
+               qf,           ctx->kind};
   hipEvent_t e0 = nullptr, e1 = nullptr;
   if (ctx->timing) {
     int rc = timing_begin(ctx, st, &e0, &e1);
     if (rc) return rc;
   }
-  const int threads = C * WAVE * wb;
-  const void* kern = sweep_kernel_ptr(ctx->K, ctx->deep_lds, ctx->klat, wb);
+  const int threads = C * WAVE;
+  const void* kern = sweep_kernel_ptr(ctx->K, ctx->deep_lds, ctx->klat);
   {
     const int* prog = ctx->d_prog;
     void* kargs[] = {(void*)&sa, (void*)&prog};
@@ -3184,9 +2979,9 @@ int launch_pattern(phy_ctx* ctx, int n, const double* d_blens, const double* d_m
   // a draw over a few workgroups: the finalize sums their slots itself
   // (one epilogue launch: slot sums, finalize, chain rule); over many, the
   // wide gsum kernel first
-  const int gsum_in = (!g_direct && gx * wb <= 16) ? 1 : 0;
+  const int gsum_in = (!g_direct && gx <= 16) ? 1 : 0;
   FinArgs fa{ctx->d_gslot, ctx->d_sslot, ctx->d_pmat, ctx->eig_cur, d_blens, d_model, ctx->d_gpos, ctx->d_inner, d_out,
-             C,            B,            ctx->nmat,   gx * wb,     phy_output_len(ctx), g_direct, ctx->R, grows, gstride,
+             C,            B,            ctx->nmat,   gx,          phy_output_len(ctx), g_direct, ctx->R, grows, gstride,
              ctx->kind,    gsum_in,      (!fin && ctx->qfuse_pref) ? 1 : 0};
   if (!g_direct && !gsum_in) {
     hipLaunchKernelGGL(gsum_kernel, dim3((C * B * 16 + 63) / 64, n), dim3(256), 0, st, fa);
@@ -3256,6 +3051,20 @@ size_t stage_small(phy_ctx* ctx, int n, const double* blens, const double* model
 }
 
 }  // namespace
+
+// Work of `body(st)` on ctx's stream, fenced both ways with the legacy null
+// stream (stream handle 0): ordered after everything queued on it before the
+// call, and everything queued on it after the call waits for it.
+template <typename F>
+int null_fenced(phy_ctx* ctx, F&& body) {
+  HIP_TRY(hipEventRecord(ctx->ev_nin, nullptr));
+  HIP_TRY(hipStreamWaitEvent(ctx->stream, ctx->ev_nin, 0));
+  const int rc = body(ctx->stream);
+  if (rc) return rc;
+  HIP_TRY(hipEventRecord(ctx->ev_nout, ctx->stream));
+  HIP_TRY(hipStreamWaitEvent(nullptr, ctx->ev_nout, 0));
+  return PHY_OK;
+}
 
 #include "multi_device.inc"
 
@@ -3337,17 +3146,10 @@ int phy_create(int S, int P, int C, int rooted, int model, const uint8_t* tipcod
     c->fin_pref = fk ? atoi(fk) != 0 : true;
     const char* qk = getenv("PHY_QFUSE");
     c->qfuse_pref = qk ? atoi(qk) != 0 : true;
-    const char* gk = getenv("PHY_GRAPH");
-    c->graph_pref = gk ? atoi(gk) != 0 : false;
-    const char* lk = getenv("PHY_KLAT");
-    c->klat_pref = lk ? atoi(lk) != 0 : true;
-    c->eig_fuse_pref = env_flag("PHY_EIG_FUSE", 1);
-    if (const char* em = getenv("PHY_EIG_FUSE_MAX")) c->eig_fuse_max = std::max(0, atoi(em));
     const char* qk2 = getenv("PHY_QUAD");
     c->quad_pref = qk2 ? atoi(qk2) != 0 : true;
     const char* qm = getenv("PHY_QMW");
     c->qmw_pref = qm ? atoi(qm) != 0 : true;
-    c->wb_pref = env_flag("PHY_WB", 0);  // opt-in: measured slower
 
   }
   hipError_t he = hipSetDevice(device);
@@ -3360,23 +3162,6 @@ int phy_create(int S, int P, int C, int rooted, int model, const uint8_t* tipcod
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess && cus > 0)
       c->cu_count = cus;
   }
-  {  // the dataflow class launch's grid: resident by construction (its items are assigned statically)
-    c->flow_pref = env_flag("PHY_FLOW", 0);  // opt-in: measured slower than the level launches
-    const int thr = C <= 4 ? 256 : 1024;
-    const void* ks[2] = {C <= 4 ? (const void*)cls_flow_kernel<256, false> : (const void*)cls_flow_kernel<1024, false>,
-                         C <= 4 ? (const void*)cls_flow_kernel<256, true> : (const void*)cls_flow_kernel<1024, true>};
-    for (int v = 0; v < 2; ++v) {
-      int nb = 0;
-      if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, ks[v], thr, 0) != hipSuccess) nb = 1;
-      // the occupancy query can over-report by one workgroup per CU (MI355X_MICROARCH.md, residency):
-      // one fewer than it says, at most 4 per CU; PHY_FLOW_WPC overrides (never above the query)
-      int wpc = std::min(4, nb >= 2 ? nb - 1 : nb);
-      const char* fw = getenv("PHY_FLOW_WPC");
-      if (fw) wpc = std::max(1, std::min(atoi(fw), std::max(nb, 1)));
-      c->flow_wgs[v] = std::max(0, wpc) * c->cu_count;
-    }
-    (void)hipGetLastError();
-  }
   // workgroup slots: an explicit budget, or up to 4 resident per CU
   c->wg_cap = (int)std::min<long>((long)c->nblk * max_draws,
                                   (long)std::max(c->wg_budget, 4 * c->cu_count) + max_draws);
@@ -3386,8 +3171,6 @@ int phy_create(int S, int P, int C, int rooted, int model, const uint8_t* tipcod
     for (int k = 0; k < 8; ++k)
       (void)hipFuncSetAttribute(sweep_kernel_ptr(1 + (k & 1), (k >> 1) & 1, (k >> 2) & 1),
                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)LDS_CAP);
-    (void)hipFuncSetAttribute(sweep_kernel_ptr(2, true, false, 2), hipFuncAttributeMaxDynamicSharedMemorySize,
-                              (int)LDS_CAP);
     (void)hipFuncSetAttribute((const void*)finalize_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)LDS_CAP);
     for (const void* kern : {(const void*)qsweep_kernel<256>, (const void*)qsweep_kernel<1024>, (const void*)qmw_kernel}) {
       hipFuncAttributes fa{};  // its static eigensystem copy counts against the cap too
@@ -3422,6 +3205,8 @@ int phy_create(int S, int P, int C, int rooted, int model, const uint8_t* tipcod
     }                                                                                \
   } while (0)
   HIP_C(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+  HIP_C(hipEventCreateWithFlags(&c->ev_nin, hipEventDisableTiming));
+  HIP_C(hipEventCreateWithFlags(&c->ev_nout, hipEventDisableTiming));
   const size_t ncolwg = (size_t)C * WAVE;
   TRY_C(dalloc(&c->d_tips, (size_t)S * c->Ppad / 2));
   TRY_C(dalloc(&c->d_w, (size_t)c->Ppad));
@@ -3443,16 +3228,6 @@ int phy_create(int S, int P, int C, int rooted, int model, const uint8_t* tipcod
     // portable: a multi-device context's shards all upload from shard 0's staging (multi_enqueue)
     HIP_C(hipHostMalloc((void**)&c->h_in, sizeof(double) * pin * (c->B + 10 + 2 * C + EIG_LEN), hipHostMallocPortable));
     HIP_C(hipHostMalloc((void**)&c->h_out, sizeof(double) * pin * outlen_full, hipHostMallocPortable));
-    if (env_flag("PHY_DIRECT_OUT", PHY_DIRECT_OUT_DEFAULT)) {
-      void* dp = nullptr;
-      HIP_C(hipHostGetDevicePointer(&dp, c->h_out, 0));
-      c->h_out_dev = static_cast<double*>(dp);
-    }
-    if (env_flag("PHY_DIRECT_IN", PHY_DIRECT_IN_DEFAULT)) {
-      void* dp = nullptr;
-      HIP_C(hipHostGetDevicePointer(&dp, c->h_in, 0));
-      c->h_in_dev = static_cast<const double*>(dp);
-    }
   }
   {
     // tip nibbles: record vector of the pattern's mask (R <= 16); padding =
@@ -3575,7 +3350,6 @@ int phy_create_multi(int S, int P, int C, int rooted, int model, const uint8_t* 
     phy_ctx* sh = nullptr;
     int rc = phy_create(S, pk, C, rooted, model, tk.data(), weights + m->p0[k], peel, max_draws, devices[k], &sh);
     if (rc) return bail(rc);
-    if (same) sh->flow_ok = false;  // same-device shards run concurrently: the flow grid could not stay resident
     m->shard.push_back(sh);
     hipEvent_t ev = nullptr;
     if (hipSetDevice(devices[k]) != hipSuccess || hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess)
@@ -3650,7 +3424,6 @@ int phy_set_output(phy_ctx* ctx, int compact) {
     if (rc) return rc;
   }
   ctx->compact = compact ? 1 : 0;
-  ++ctx->plan_gen;
   return PHY_OK;
 }
 
@@ -3673,26 +3446,22 @@ int phy_eval_device(phy_ctx* ctx, int n_draws, const double* d_blens, const doub
   if (ctx->pending)  // the submitted evaluation still uses the context's work buffers
     return fail(PHY_EINVAL, "phy_eval_device: a phy_eval_submit is still in flight (phy_eval_wait first)");
   HIP_TRY(hipSetDevice(ctx->device));
-  hipStream_t st = stream ? reinterpret_cast<hipStream_t>(stream) : ctx->stream;
-  return launch_graphed(ctx, n_draws, d_blens, d_model, d_out, d_site_ll, st,
-                        [&]() -> int { return launch(ctx, n_draws, d_blens, d_model, d_out, d_site_ll, st); });
+  if (stream) return launch(ctx, n_draws, d_blens, d_model, d_out, d_site_ll, reinterpret_cast<hipStream_t>(stream));
+  // NULL: the caller's legacy null stream (a HIP / torch default-stream caller,
+  // prune_stan.hpp:9-17's synchronous contract): the evaluation runs on the
+  // context's stream, after the null stream's earlier work and before its later
+  return null_fenced(ctx, [&](hipStream_t st) { return launch(ctx, n_draws, d_blens, d_model, d_out, d_site_ll, st); });
 }
 
-// The small-batch path's launches: inputs staged in h_in (stage_small),
-// rows to h_out.  With PHY_DIRECT_IN / PHY_DIRECT_OUT the kernels read the
-// staged inputs from / write the rows to pinned host memory themselves
-// instead of a blit each way.
+// The small-batch path's launches: inputs staged in h_in (stage_small), one
+// blit in, the launches, the rows to h_out (one blit out).
 int launch_small(phy_ctx* ctx, int n_draws, size_t nin, size_t nb, size_t nm, size_t no, bool heig, double* dsite,
                  hipStream_t st) {
-  const double* in = ctx->h_in_dev;
-  if (!in) {
-    HIP_TRY(hipMemcpyAsync(ctx->d_in, ctx->h_in, sizeof(double) * nin, hipMemcpyHostToDevice, st));
-    in = ctx->d_in;
-  }
-  double* out = ctx->h_out_dev ? ctx->h_out_dev : ctx->d_out;
-  int r = launch(ctx, n_draws, in, in + nb, out, dsite, st, heig ? in + nb + nm : nullptr);
+  HIP_TRY(hipMemcpyAsync(ctx->d_in, ctx->h_in, sizeof(double) * nin, hipMemcpyHostToDevice, st));
+  const double* in = ctx->d_in;
+  int r = launch(ctx, n_draws, in, in + nb, ctx->d_out, dsite, st, heig ? in + nb + nm : nullptr);
   if (r) return r;
-  if (!ctx->h_out_dev) HIP_TRY(hipMemcpyAsync(ctx->h_out, ctx->d_out, sizeof(double) * no, hipMemcpyDeviceToHost, st));
+  HIP_TRY(hipMemcpyAsync(ctx->h_out, ctx->d_out, sizeof(double) * no, hipMemcpyDeviceToHost, st));
   return PHY_OK;
 }
 
@@ -3722,9 +3491,7 @@ int phy_eval_submit(phy_ctx* ctx, int n_draws, const double* blens, const double
   const size_t no = (size_t)n_draws * phy_output_len(ctx);
   bool heig = false;
   const size_t nin = stage_small(ctx, n_draws, blens, model, &heig);
-  int rc = launch_graphed(ctx, n_draws, ctx->h_in, ctx->d_in, ctx->h_out, nullptr, st, [&]() -> int {
-    return launch_small(ctx, n_draws, nin, nb, nm, no, heig, nullptr, st);
-  });
+  int rc = launch_small(ctx, n_draws, nin, nb, nm, no, heig, nullptr, st);
   if (rc) return rc;
   ctx->pending = n_draws;
   return PHY_OK;
@@ -3765,9 +3532,7 @@ int phy_eval(phy_ctx* ctx, int n_draws, const double* blens, const double* model
     bool heig = false;
     const size_t nin = stage_small(ctx, n_draws, blens, model, &heig);
     double* dsite = site_ll ? ctx->d_site : nullptr;
-    int rc = launch_graphed(ctx, n_draws, ctx->h_in, ctx->d_in, ctx->h_out, dsite, st, [&]() -> int {
-      return launch_small(ctx, n_draws, nin, nb, nm, no, heig, dsite, st);
-    });
+    int rc = launch_small(ctx, n_draws, nin, nb, nm, no, heig, dsite, st);
     if (rc) return rc;
     if (site_ll)
       HIP_TRY(hipMemcpyAsync(site_ll, ctx->d_site, sizeof(double) * n_draws * ctx->P, hipMemcpyDeviceToHost, st));
@@ -3906,19 +3671,6 @@ int phy_set_recompute(phy_ctx* ctx, int on) {
 }
 int phy_recomputed_partials(const phy_ctx* ctx) { return ctx ? (ctx->ms ? ctx->ms->shard[0]->nrec : ctx->nrec) : -1; }
 
-int phy_set_graphs(phy_ctx* ctx, int on) {
-  if (!ctx) return fail(PHY_EINVAL, "NULL ctx");
-  if (ctx->ms) {  // the shards launch direct; the flag is kept for phy_eval_* on this context
-    ctx->graph_pref = on != 0;
-    return PHY_OK;
-  }
-  HIP_TRY(hipSetDevice(ctx->device));
-  HIP_TRY(hipStreamSynchronize(ctx->stream));
-  ctx->graph_pref = on != 0;
-  ++ctx->plan_gen;
-  return PHY_OK;
-}
-
 int phy_set_engine(phy_ctx* ctx, int mode) {
   if (!ctx) return fail(PHY_EINVAL, "NULL ctx");
   if (ctx->ms) {  // every shard
@@ -3936,26 +3688,6 @@ int phy_set_engine(phy_ctx* ctx, int mode) {
   HIP_TRY(hipStreamSynchronize(ctx->stream));
   ctx->engine_pref = mode;
   return select_engine(ctx);
-}
-
-int phy_set_flow(phy_ctx* ctx, int on) {
-  if (!ctx) return fail(PHY_EINVAL, "NULL ctx");
-  if (ctx->ms) {
-    for (phy_ctx* sh : ctx->ms->shard) {
-      int rc = phy_set_flow(sh, on);
-      if (rc) return rc;
-    }
-    return PHY_OK;
-  }
-  ctx->flow_pref = on != 0;
-  ++ctx->plan_gen;
-  return PHY_OK;
-}
-
-int phy_flow(const phy_ctx* ctx) {
-  if (!ctx) return -1;
-  if (ctx->ms) return phy_flow(ctx->ms->shard[0]);
-  return (ctx->engine == 1 && flow_applies(ctx)) ? 1 : 0;
 }
 
 int phy_engine(const phy_ctx* ctx) { return ctx ? (ctx->ms ? ctx->ms->shard[0]->engine : ctx->engine) : -1; }
@@ -4024,7 +3756,7 @@ int phy_lds_plan(const phy_ctx* ctx, int* n_chunks, int* matrices_per_chunk, int
   if (n_chunks) *n_chunks = ctx->nchunks;  // matrix-record chunks per pass
   if (matrices_per_chunk) *matrices_per_chunk = ctx->cap_m;
   if (lds_bytes_out)
-    *lds_bytes_out = (int)lds_bytes(ctx->S, ctx->C, ctx->R, ctx->cap_m, ctx->K, ctx->ndl, ctx->wb);
+    *lds_bytes_out = (int)lds_bytes(ctx->S, ctx->C, ctx->R, ctx->cap_m, ctx->K, ctx->ndl);
   return PHY_OK;
 }
 

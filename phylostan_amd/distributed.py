@@ -6,8 +6,14 @@ count-balanced range of patterns and evaluates its shard with its own
 dL/dP, branch / rate / mixture / root-frequency gradients) is a sum over
 patterns, so a single ``all_reduce(SUM)`` of that vector -- over RCCL
 (``torch.distributed`` backend "nccl" on ROCm) between MI355X GPUs on xGMI --
-is the whole exchange: for S = 128, C = 4 it is 1 + 254 + 12 + 16*4*254
-doubles = 130 KB per draw, latency-bound on xGMI.
+is the whole exchange.  With ``compact=True`` (what a sampler consumes: the
+log-likelihood and every parameter gradient -- branch lengths, rates,
+mixture weights, exchangeabilities, frequencies) the rows stop before the
+dL/dP block: for S = 128, C = 4 that is 1 + 254 + 8 + 14 doubles = 2.2 KB
+per draw instead of 132 KB with the block (1 + 254 + 8 + 14 + 16*4*254
+doubles).  The model-parameter gradients are linear in dL/dP and the root
+term, so the compact rows of the shards sum to the compact rows of the
+whole (tests/test_distributed.py).
 
 The reference has no distributed code at all (SURVEY.md 2, "Parallelism");
 this module is the build's addition.  ``engine_factory`` lets the CPU tests
@@ -48,7 +54,7 @@ class ShardedLikelihood:
     """
 
     def __init__(self, tipcodes, weights, peel0, rooted, model, C, rank, world, device=0,
-                 max_draws=1, engine_factory=None):
+                 max_draws=1, engine_factory=None, compact=False):
         self.rank, self.world = rank, world
         P = np.asarray(tipcodes).shape[1]
         self.p0, self.p1 = shard_range(P, rank, world)
@@ -61,6 +67,9 @@ class ShardedLikelihood:
         self.engine = engine_factory(np.ascontiguousarray(np.asarray(tipcodes)[:, self.p0:self.p1]),
                                      np.ascontiguousarray(np.asarray(weights)[self.p0:self.p1]),
                                      peel0, rooted, model, C, max_draws=max_draws, device=device)
+        if compact:
+            self.engine.set_output(compact=True)
+        self._side = {}  # per device: the side stream that fences a null-stream caller
 
     @property
     def outlen(self):
@@ -74,9 +83,9 @@ class ShardedLikelihood:
         orders itself against, so the reduction reads ``out`` only after the
         kernels wrote it and the kernels read blens / model only after torch
         produced them.  torch's default stream is the null stream (handle 0),
-        which the C boundary reads as "the context's own stream"
-        (include/phylo_hip.h phy_eval_device): on it the sweep runs on a side
-        stream fenced both ways with events instead.
+        which the C boundary fences itself (include/phylo_hip.h
+        phy_eval_device); the side stream here, fenced both ways with events,
+        keeps that ordering explicit on torch's side as well.
         """
         import torch
         import torch.distributed as dist
@@ -87,11 +96,14 @@ class ShardedLikelihood:
             stream = torch.cuda.current_stream(out.device).cuda_stream
         if out.is_cuda and not stream:
             cur = torch.cuda.current_stream(out.device)
-            if getattr(self, "_side", None) is None:
-                self._side = torch.cuda.Stream(device=out.device)
-            self._side.wait_stream(cur)
-            self.engine.evaluate_device(*args, n_draws=n, stream=self._side.cuda_stream)
-            cur.wait_stream(self._side)
+            side = self._side.get(out.device)
+            if side is None:
+                side = self._side[out.device] = torch.cuda.Stream(device=out.device)
+            side.wait_stream(cur)
+            self.engine.evaluate_device(*args, n_draws=n, stream=side.cuda_stream)
+            for t in (blens, model, out) + ((site_ll,) if site_ll is not None else ()):
+                t.record_stream(side)  # the caching allocator must not reuse them before the side stream is done
+            cur.wait_stream(side)
         else:
             self.engine.evaluate_device(*args, n_draws=n, stream=stream)
         if self.world > 1:

@@ -242,17 +242,13 @@ class TreeLikelihood:
 
     def set_tuning(self, wg_budget=0, cols=0, lds_budget=0):
         """Persistent-workgroup budget, columns per lane (0 = automatic, 1, 2)
-        and LDS bytes per workgroup (0 = keep); see include/phylo_hip.h."""
+        and LDS bytes per workgroup (0 = keep); see include/phylo_hip_diag.h."""
         _lib.check(self.lib.phy_set_tuning(self.ctx, int(wg_budget), int(cols), int(lds_budget)),
                    "phy_set_tuning")
 
     def set_deep_stack(self, mode=0):
         """Deep-stack placement: 0 automatic, 1 LDS, 2 global (replans)."""
         _lib.check(self.lib.phy_set_deep_stack(self.ctx, int(mode)), "phy_set_deep_stack")
-
-    def set_graphs(self, on=True):
-        """Replay repeated evaluations from HIP graphs (phy_set_graphs)."""
-        _lib.check(self.lib.phy_set_graphs(self.ctx, int(bool(on))), "phy_set_graphs")
 
     def set_recompute(self, on=True):
         """Rebuild cherries in the reverse half instead of storing them (replans)."""
@@ -318,16 +314,6 @@ class TreeLikelihood:
         self.set_engine(min(med, key=med.get))
         return self.engine()
 
-    def set_flow(self, on=True):
-        """The class sweep as ONE dataflow launch (opt-in) or one launch per
-        tree level and phase (default, measured faster); phy_set_flow;
-        bitwise the same results."""
-        _lib.check(self.lib.phy_set_flow(self.ctx, int(bool(on))), "phy_set_flow")
-
-    def flow(self):
-        """True when the next class-sweep launch is the dataflow one."""
-        return self.lib.phy_flow(self.ctx) == 1
-
     def engine(self):
         """The engine the next launch uses: "pattern" or "class"."""
         return ("pattern", "class")[self.lib.phy_engine(self.ctx)]
@@ -354,7 +340,7 @@ class TreeLikelihood:
 
     def quad_plan(self):
         """The small-call sweep's plan: waves per category, schedule length in
-        program steps, LDS hand-off slots (include/phylo_hip.h phy_quad_plan)."""
+        program steps, LDS hand-off slots (include/phylo_hip_diag.h phy_quad_plan)."""
         w, sp, sl = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
         _lib.check(self.lib.phy_quad_plan(self.ctx, ctypes.byref(w), ctypes.byref(sp), ctypes.byref(sl)),
                    "phy_quad_plan")

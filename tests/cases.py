@@ -127,6 +127,26 @@ def ds1_case(seed=0):
                 np.full(4, 0.25), np.ones(6), [1.0], [1.0])
 
 
+def ds1_topology_case(k):
+    """Config 1 on DS1 topology k of the 42 in examples/DS1/DS1.trees (the
+    reference pipeline's tree{k}.tree, examples/SConstruct:159-188): its
+    layout from the reference's utils.py and the blens of its reference
+    per-site log-likelihoods (tests/golden/DS1_topologies.npz)."""
+    d = np.load(os.path.join(GOLDEN, "DS1_topologies.npz"), allow_pickle=False)
+    tip = d["tipbits0"][d["perm"][k]]
+    j = int(np.nonzero(d["ll_topologies"] == k)[0][0])
+    return Case("DS1_tree%d" % k, tip, d["weights"], d["peel"][k] - 1, False, "JC69", 1, d["blens"][j],
+                np.full(4, 0.25), np.ones(6), [1.0], [1.0])
+
+
+def ds1_topology_reference(k):
+    """The reference's (scripts/phylo.py) per-pattern log-likelihoods and total
+    for DS1 topology k at ds1_topology_case(k)'s branch lengths."""
+    d = np.load(os.path.join(GOLDEN, "DS1_topologies.npz"), allow_pickle=False)
+    j = int(np.nonzero(d["ll_topologies"] == k)[0][0])
+    return d["site_ll"][j], float(d["loglik"][j])
+
+
 def kat_case(point):
     """3-taxon KAT of eigen/test_ll_3tax.py in Stan JC69 units (b = 0.75 t)."""
     b14, b24, b45, b35 = point["branches_b14_b24_b45_b35"]

@@ -32,6 +32,10 @@ What is taken from the reference (nothing here is restated by us):
   (``phylostan_amd/treeio.py``); ``numpy.int`` (removed in numpy >= 1.24) is
   re-bound to ``int`` for the call.  ``tipdata`` (0/1 ``[S, L, 4]``) is
   stored losslessly as bit masks ``sum_k tipdata[..., k] << k``.
+* ``DS1_topologies.npz`` -- config 1 over all 42 topologies of
+  ``examples/DS1/DS1.trees``, as ``examples/SConstruct:159-188`` runs it:
+  each topology's layout from ``utils.py`` and its per-site
+  log-likelihoods from ``scripts/phylo.py`` (``ds1_topologies_fixture``).
 """
 import json
 import os
@@ -560,6 +564,73 @@ def zero_rate_fixture(phylo, specs):
     return out
 
 
+DS1_LL_TOPOLOGIES = tuple(range(42))  # every topology gets reference per-site log-likelihoods
+
+
+def ds1_topologies_fixture(utils, phylo):
+    """Config 1 as the reference's pipeline runs it (examples/SConstruct:159-188):
+    DS1.trees split into its 42 topologies, `phylostan run -m JC69` on each.
+    For every line, the Stan data layout from the reference's own
+    phylostan/utils.py (layout_fixture: peel with the unrooted swap of
+    phylostan.py:264-267, map), the taxon-namespace order as a permutation of
+    topology 0's (the compressed patterns do not depend on the row order:
+    tipbits_k = tipbits_0[perm_k], checked here), and for every topology
+    the per-pattern log-likelihoods of the reference's scripts/phylo.py pruner
+    under the unrooted convention (the edge to node 2S-3 zeroed:
+    generate_script.py:1019 and the pulley principle; normalised JC69) with
+    blens ~ Exp(10), seed 1000 + k."""
+    import tempfile
+    from phylostan_amd import data
+    tpath = os.path.join(REF, "examples", "DS1", "DS1.trees")
+    apath = os.path.join(REF, "examples", "DS1", "DS1.nex")
+    lines = [ln.rstrip("\n").rstrip("\r") for ln in open(tpath) if ln.strip()]
+    aln = treeio.read_alignment(apath)
+    out = {"peel": [], "map": [], "perm": [], "ll_topologies": list(DS1_LL_TOPOLOGIES), "blens": [], "site_ll": [],
+           "loglik": []}
+    taxa0 = tip0 = None
+    with tempfile.TemporaryDirectory() as td:
+        for k, line in enumerate(lines):
+            tf = os.path.join(td, "tree%d.tree" % k)
+            with open(tf, "w") as fp:
+                fp.write(line)
+            fx = layout_fixture(utils, tf, apath, False, False)
+            taxa = [str(t) for t in fx["taxa"]]
+            if k == 0:
+                taxa0, tip0 = taxa, fx["tipbits"]
+                out["taxa0"] = taxa0
+                out["tipbits0"] = tip0
+                out["weights"] = fx["weights"]
+            perm = np.array([taxa0.index(t) for t in taxa], dtype=np.int32)
+            assert np.array_equal(fx["tipbits"], tip0[perm]), "patterns depend on the row order"
+            out["peel"].append(fx["peel"])
+            out["map"].append(fx["map"])
+            out["perm"].append(perm)
+            if k in DS1_LL_TOPOLOGIES:
+                tree = treeio.read_tree(tf)
+                tree.resolve_polytomies(update_bipartitions=True)
+                rows = {t.label: _Seq(aln[t.label]) for t in tree.taxon_namespace}
+                alignment = _Alignment(rows)
+                S = len(alignment)
+                phylo.setup_indexes(tree, alignment)
+                peel0 = fx["peel"] - 1
+                assert peel0[-1][1] == 2 * S - 3
+                blens = np.random.default_rng(1000 + k).exponential(1.0 / 10.0, size=2 * S - 3)
+                for nd in tree.postorder_node_iter():
+                    if nd.parent_node is not None:
+                        nd.edge_length = 0.0 if nd.index == 2 * S - 3 else float(blens[nd.index])
+                site = np.log(_phylo_root_site_lik(phylo, tree, alignment, phylo.GTR([1.0] * 6, [0.25] * 4)))
+                chars = np.array([[ord(ch) for ch in str(rows[t]).upper()] for t in taxa], dtype=np.uint8)
+                _, _, first = data.compress_patterns(chars)
+                out["blens"].append(blens)
+                out["site_ll"].append(site[first])
+                out["loglik"].append(float(np.sum(site)))
+                print("DS1 topology %d JC69 unrooted reference loglik %.10f" % (k, np.sum(site)))
+    return {"peel": np.stack(out["peel"]), "map": np.stack(out["map"]), "perm": np.stack(out["perm"]),
+            "taxa0": np.array(out["taxa0"]), "tipbits0": out["tipbits0"], "weights": out["weights"],
+            "ll_topologies": np.array(out["ll_topologies"], dtype=np.int32), "blens": np.stack(out["blens"]),
+            "site_ll": np.stack(out["site_ll"]), "loglik": np.array(out["loglik"])}
+
+
 def main():
     if len(sys.argv) > 1 and sys.argv[1] == "zero_rate":  # only the site-rate variants' fixture
         ex = os.path.join(REF, "examples")
@@ -575,6 +646,10 @@ def main():
                  "DS1": (os.path.join(ex, "DS1", "DS1.trees"), os.path.join(ex, "DS1", "DS1.nex"))}
         with open(os.path.join(HERE, "phylo_grad.json"), "w") as fp:
             json.dump(grad_fixture(_import_reference_phylo(), specs), fp, indent=1)
+        return
+    if len(sys.argv) > 1 and sys.argv[1] == "ds1_topologies":  # only the 42 DS1 topologies
+        np.savez_compressed(os.path.join(HERE, "DS1_topologies.npz"),
+                            **ds1_topologies_fixture(_import_reference_utils(), _import_reference_phylo()))
         return
     if len(sys.argv) > 1 and sys.argv[1] == "mixture":  # only the mixture / unrooted fixture
         ex = os.path.join(REF, "examples")
@@ -602,6 +677,7 @@ def main():
         json.dump(phylo_gtr_fixture(utils, phylo, specs), fp)
     with open(os.path.join(HERE, "phylo_mixture.json"), "w") as fp:
         json.dump(mixture_fixture(phylo, specs), fp)
+    np.savez_compressed(os.path.join(HERE, "DS1_topologies.npz"), **ds1_topologies_fixture(utils, phylo))
 
 
 if __name__ == "__main__":

@@ -1,5 +1,6 @@
 """CPU: the C-ABI library builds, loads and exports exactly what
-include/phylo_hip.h declares; without a GPU the product fails loudly."""
+include/phylo_hip.h (the consumer boundary) and include/phylo_hip_diag.h
+(planning / introspection) declare; without a GPU the product fails loudly."""
 import ctypes
 import os
 import re
@@ -8,19 +9,24 @@ import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 HEADER = os.path.join(ROOT, "include", "phylo_hip.h")
+DIAG_HEADER = os.path.join(ROOT, "include", "phylo_hip_diag.h")
 
 
-def declared_functions():
-    text = open(HEADER).read()
-    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
-    return sorted(set(re.findall(r"\b(phy_[a-z_]+)\s*\(", text)))
+def declared_functions(headers=(HEADER, DIAG_HEADER)):
+    names = set()
+    for h in headers:
+        text = re.sub(r"/\*.*?\*/", "", open(h).read(), flags=re.S)
+        names.update(re.findall(r"\b(phy_[a-z_]+)\s*\(", text))
+    return sorted(names)
 
 
 def test_header_declares_the_boundary():
-    names = declared_functions()
-    for required in ("phy_create", "phy_destroy", "phy_eval", "phy_eval_device", "phy_pruning_loglik",
-                     "phy_last_error"):
-        assert required in names
+    names = declared_functions((HEADER,))
+    assert names == sorted(["phy_create", "phy_create_multi", "phy_destroy", "phy_last_error", "phy_num_branches",
+                            "phy_output_len", "phy_eval", "phy_eval_device", "phy_eval_submit", "phy_eval_wait",
+                            "phy_pruning_loglik", "phy_sync", "phy_set_output"])
+    diag = declared_functions((DIAG_HEADER,))
+    assert not set(names) & set(diag)
 
 
 def test_library_exports_every_declared_symbol():

@@ -10,8 +10,8 @@ import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 def latest(kind):
-    """The newest round's committed line of this kind (r05_..., else r04_..., r03_...)."""
-    for r in ("r05", "r04", "r03"):
+    """The newest round's committed line of this kind (r06_..., else r05_..., r04_..., r03_...)."""
+    for r in ("r06", "r05", "r04", "r03"):
         if os.path.exists(os.path.join(ROOT, "profiles", "%s_%s" % (r, kind))):
             return "%s_%s" % (r, kind)
     raise FileNotFoundError(kind)
@@ -115,3 +115,32 @@ def test_default_line_reports_the_one_draw_sampler_call():
         pytest.skip("the committed fluA line predates the 1-draw figure")
     assert 0 < sl["pattern_us_per_call_1draw"] < 1e4
     assert d["draws_100"] is not None
+
+
+def _check_counted(hbm, traffic, alg, kern_ms):
+    if traffic is None:
+        assert hbm["counted_gbps"] is None and hbm["counted_frac"] is None
+        return
+    g = traffic / (kern_ms * 1e-3) / 1e9
+    assert hbm["counted_gbps"] == pytest.approx(g, rel=1e-12)
+    assert hbm["counted_frac"] == pytest.approx(g / 8000.0, rel=1e-12)
+    assert hbm["traffic_over_algorithmic"] == pytest.approx(traffic / alg, rel=1e-12)
+    assert ("below" in hbm["counted_note"]) == (traffic < alg)
+
+
+def test_default_line_reports_counted_hbm_and_all_thread_baselines():
+    """the rocprof-counted HBM rate (PMC bytes per launch
+    over the kernel's average launch) beside the algorithmic one, for fluA and
+    synthetic, a note when counted bytes are below algorithmic, and the
+    synthetic record's OpenMP CPU baseline on the job's threads."""
+    d = last_line(latest("fluA_bench.json"))
+    rf = d["roofline"]
+    if "counted_gbps" not in rf.get("hbm", {}):
+        pytest.skip("the committed fluA line predates the counted HBM rate")
+    _check_counted(rf["hbm"], rf["traffic"], rf["hbm"]["algorithmic_bytes_per_launch"], rf["kernel_avg_ms"])
+    sy = d["synthetic"]
+    srf = sy["roofline"]
+    _check_counted(srf["hbm"], srf["traffic"], srf["algorithmic_bytes_per_launch"], srf["kernel_avg_ms"])
+    mt = sy["cpu_baseline_all_threads"]
+    assert mt["kind"] == "port" and mt["cores"] > 1 and mt["unit"] == "evals/s" and mt["value"] > 0
+    assert d["cpu_baseline_all_threads"]["cores"] == mt["cores"]

@@ -31,6 +31,10 @@ class OracleShardEngine:
         self.C = C
         self.outlen = 1 + self.B + 2 * C + 4 + 10 + 16 * C * self.B
 
+    def set_output(self, compact=False):
+        """compact rows: the full row without its dL/dP block (phy_set_output)."""
+        self.outlen = 1 + self.B + 2 * self.C + 4 + 10 + (0 if compact else 16 * self.C * self.B)
+
     def evaluate_device(self, d_blens, d_model, d_out, d_site_ll=0, n_draws=1, stream=0):
         from oracle import cpu
         tip, w, peel, rooted, kind, C = self.args
@@ -42,13 +46,13 @@ class OracleShardEngine:
             ctypes.memmove(d_out + 8 * k * self.outlen, out.ctypes.data, 8 * self.outlen)
 
 
-def _worker(rank, world, port, case_args, result_q):
+def _worker(rank, world, port, case_args, result_q, compact=False):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     case = cases.random_case(*case_args[0], **case_args[1])
     sl = ShardedLikelihood(case.tipcodes, case.weights, case.peel0, case.rooted, case.model, case.C,
-                           rank, world, max_draws=2, engine_factory=OracleShardEngine)
+                           rank, world, max_draws=2, engine_factory=OracleShardEngine, compact=compact)
     blens = torch.tensor(np.stack([case.blens, case.blens * 1.3]))
     model = torch.tensor(np.stack([case.model_vec(), case.model_vec()]))
     out = torch.zeros((2, sl.outlen), dtype=torch.float64)
@@ -65,19 +69,24 @@ def _free_port():
         return s.getsockname()[1]
 
 
-@pytest.mark.parametrize("world", [2])
-def test_sharded_allreduce_equals_full(world):
-    case_args = ((4,), dict(S=11, P=97, C=3, model="GTR", rooted=True))
+def _run_sharded(world, case_args, compact):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, case_args, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, case_args, q, compact)) for r in range(world)]
     for p in procs:
         p.start()
     got = q.get(timeout=120)
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
+    return got
+
+
+@pytest.mark.parametrize("world", [2])
+def test_sharded_allreduce_equals_full(world):
+    case_args = ((4,), dict(S=11, P=97, C=3, model="GTR", rooted=True))
+    got = _run_sharded(world, case_args, compact=False)
     case = cases.random_case(*case_args[0], **case_args[1])
     eng = OracleShardEngine(case.tipcodes, case.weights, case.peel0, True, case.model, case.C)
     for k, scale in enumerate((1.0, 1.3)):
@@ -86,6 +95,28 @@ def test_sharded_allreduce_equals_full(world):
                                case.blens * scale, case.C)
         np.testing.assert_allclose(got[k], full, rtol=1e-11, atol=1e-11 * np.abs(full).max())
     assert eng.outlen == got.shape[1]
+
+
+def test_sharded_compact_allreduce_equals_compact_rows_of_full_sum():
+    """The sampler's collective (compact rows: log-lik and every parameter
+    gradient, no dL/dP block -- 2.2 KB instead of 132 KB per draw at the
+    synthetic config): the all-reduced compact rows of two pattern shards
+    equal the compact part of the all-reduced full rows, and the whole
+    alignment's rows.  The exchangeability / frequency gradients are linear
+    in dL/dP and the root term, so they sum across shards like the rest."""
+    case_args = ((4,), dict(S=11, P=97, C=3, model="GTR", rooted=True))
+    full = _run_sharded(2, case_args, compact=False)
+    comp = _run_sharded(2, case_args, compact=True)
+    case = cases.random_case(*case_args[0], **case_args[1])
+    B, C = 2 * case.tipcodes.shape[0] - 2, case.C
+    G = 1 + B + 2 * C + 14
+    assert comp.shape == (2, G) and full.shape[1] == G + 16 * C * B
+    np.testing.assert_allclose(comp, full[:, :G], rtol=1e-13, atol=1e-13 * np.abs(full[:, :G]).max())
+    from oracle import cpu
+    for k, scale in enumerate((1.0, 1.3)):
+        whole, _ = cpu.evaluate(case.tipcodes, case.weights, case.peel0, True, 2, case.model_vec(),
+                                case.blens * scale, case.C)
+        np.testing.assert_allclose(comp[k], whole[:G], rtol=1e-11, atol=1e-11 * np.abs(whole[:G]).max())
 
 
 def test_shard_ranges_cover_and_balance():

@@ -485,30 +485,3 @@ def test_retired_resident_engine_is_refused():
         eng.set_engine(3)
     assert eng.engine() == "pattern"
 
-
-def test_block_wave_plan_rows_equal(monkeypatch):
-    """The opt-in block-wave plan (PHY_WB=1: a workgroup of C x 2 waves runs
-    two pattern blocks over one LDS chunk holding every matrix record) forms
-    the same terms as the default plan; its per-draw partial sums (dL/dP,
-    scalars) meet in another order (block-wave slots summed by the epilogue
-    instead of one wave's running sum), so every output row of a 256-draw
-    fluA launch agrees with the default plan's to a few ulps, not bit for
-    bit."""
-    from phylostan_amd import models
-    from phylostan_amd.engine import TreeLikelihood
-    base = cases.fluA_case()
-    n = 256
-    rng = np.random.default_rng(29)
-    blens = base.blens[None, :] * rng.uniform(0.6, 1.4, (n, base.blens.size))
-    mvs = np.stack([models.model_vector(base.freqs, models.hky_exchangeabilities(rng.uniform(3.0, 8.0)), base.rs,
-                                        base.ps) for _ in range(n)])
-    rows = {}
-    for wb in ("0", "1"):
-        monkeypatch.setenv("PHY_WB", wb)
-        eng = TreeLikelihood(base.tipcodes, base.weights, base.peel0, True, "HKY", 4, max_draws=n)
-        plan = eng.lds_plan()
-        assert plan["n_chunks"] == (1 if wb == "1" else 2), plan
-        rows[wb] = eng.evaluate_rows(blens, mvs)
-    a, b = rows["0"], rows["1"]
-    scale = np.maximum(np.abs(a).max(axis=0), 1e-300)
-    assert np.max(np.abs(a - b) / scale) < 1e-12

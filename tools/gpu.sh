@@ -5,7 +5,7 @@
 # items are `base` (this build), a variant library `variants/x.so` (loaded with
 # PHYLO_HIP_AB=1 PHYLO_HIP_LIB), or environment settings `K=V[,K=V...]` for
 # this build; they alternate the variants, two rounds (AB_REPS):
-#   AB_VARIANTS="base variants/x.so PHY_WB=1" AB_ARGS="--workload synthetic --shard-of 8" tools/gpu.sh T ab
+#   AB_VARIANTS="base variants/x.so PHY_PAIR=0" AB_ARGS="--workload synthetic --shard-of 8" tools/gpu.sh T ab
 #   AB_VARIANTS="base variants/x.so" LAT_WLS="fluA HCV" LAT_DRAWS="4 100" tools/gpu.sh T latab
 #   tools/gpu.sh T infer | draws | ldsenv     (the round-2/3 inference, draws-per-launch and LDS-plan runs)
 # Every GPU step has its own time limit and the steps are chained: the first
@@ -23,21 +23,6 @@ step_tests() {
     > $O/pytest.log 2>&1 || { tail -30 $O/pytest.log; exit 1; }
   tail -40 $O/pytest.log
 }
-step_tests5() {  # this round's new GPU tests only
-  timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 800 --timeout-method thread \
-    -k "zero_rate or config3" > $O/pytest5.log 2>&1 || { tail -30 $O/pytest5.log; exit 1; }
-  tail -12 $O/pytest5.log
-}
-step_flow() {  # the dataflow class launch: bitwise against the level launches, stress, then the class suite
-  timeout -k 10 600 python -u -m pytest tests/test_gpu_class.py -x -v --timeout 240 --timeout-method thread \
-    > $O/pytest_flow.log 2>&1 || { tail -40 $O/pytest_flow.log; exit 1; }
-  tail -12 $O/pytest_flow.log
-}
-step_stress() {  # the relaxed hand-off stress tests: 10^4 calls each, outputs bitwise (quad epilogue, class flow)
-  timeout -k 10 600 python -u -m pytest tests/test_gpu_quad.py tests/test_gpu_class.py -x -v -k stress --timeout 400 \
-    --timeout-method thread > $O/pytest_stress.log 2>&1 || { tail -30 $O/pytest_stress.log; exit 1; }
-  tail -6 $O/pytest_stress.log
-}
 step_smoke() {
   timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1
   tail -3 $O/smoke.log
@@ -50,34 +35,6 @@ step_rehearse() {  # the N = 2 path of the default run on the one GPU (gloo, bot
   timeout -k 10 500 python bench.py --gpus 2 --rehearse --steps 20 --warmup 5 --json-out $O/bench_rehearse2.json \
     > $O/bench_rehearse2.log 2>&1 || { tail -30 $O/bench_rehearse2.log; exit 1; }
   tail -c 2500 $O/bench_rehearse2.json
-}
-step_flowtrace() {  # the dataflow class launch's per-item trace (shard of 8, one GPU), and the level launches beside it
-  rm -f $O/ft.bin
-  PHY_FLOW=1 PHY_FLOW_TRACE=$O/ft.bin timeout -k 10 300 python bench.py --workload synthetic --shard-of 8 --steps 3 --warmup 1 \
-    --no-cpu-baseline --json-out $O/bench_ft.json > $O/bench_ft.log 2>&1
-  python tools/flow_trace.py $O/ft.bin
-  for w in 3 4; do
-    PHY_FLOW=1 PHY_FLOW_WPC=$w timeout -k 10 300 python bench.py --workload synthetic --shard-of 8 --steps 100 --warmup 10 \
-      --no-cpu-baseline --json-out $O/bench_shard8_w$w.json > $O/bench_shard8_w$w.log 2>&1
-    python -c "import json;d=json.load(open('$O/bench_shard8_w$w.json'));print('shard8 flow wpc $w', d['value'], d['ms_per_step'])"
-  done
-  PHY_FLOW=0 timeout -k 10 300 python bench.py --workload synthetic --shard-of 8 --steps 100 --warmup 10 \
-    --no-cpu-baseline --json-out $O/bench_shard8_lvl.json > $O/bench_shard8_lvl.log 2>&1
-  python -c "import json;d=json.load(open('$O/bench_shard8_lvl.json'));print('shard8 level launches', d['value'], d['ms_per_step'])"
-}
-step_cfg3dbg() {  # config 3 alone, with a stack dump if it hangs
-  timeout -k 10 300 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread \
-    -k "config3" > $O/pytest_cfg3.log 2>&1 || { tail -80 $O/pytest_cfg3.log; exit 1; }
-  tail -5 $O/pytest_cfg3.log
-}
-step_wbab() {  # block-wave plan (PHY_WB, default on) against the one-block-wave plan, alternating, fluA batched
-  for r in 1 2; do
-    for w in 1 0; do
-      PHY_WB=$w timeout -k 10 200 python bench.py --steps 100 --warmup 10 --no-cpu-baseline --no-sampler-latency \
-        --no-synthetic --json-out $O/bench_wb${w}_$r.json > $O/bench_wb${w}_$r.log 2>&1
-      python -c "import json;d=json.load(open('$O/bench_wb${w}_$r.json'));print('PHY_WB=$w', d['value'], d['roofline']['kernel_avg_ms'], d['program'])"
-    done
-  done
 }
 step_parity() {  # the parity suites of the pattern sweep (every plan) and the configs
   timeout -k 10 600 python -u -m pytest tests/test_gpu_00_configs.py tests/test_gpu_parity.py tests/test_gpu_large_cb.py \
