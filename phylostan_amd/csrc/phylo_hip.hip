@@ -3273,10 +3273,12 @@ int phy_create(int S, int P, int C, int rooted, int model, const uint8_t* tipcod
       const std::vector<int> qp = quad_program(c->prog, c->nsteps, C, c->R);
       TRY_C(dalloc(&c->d_qprog, qp.size()));
       HIP_C(hipMemcpy(c->d_qprog, qp.data(), qp.size() * sizeof(int), hipMemcpyHostToDevice));
-      // the multi-wave variant: as many waves per category as a 1024-thread workgroup holds (<= 4)
-      const int W = std::min(QMW_MAXW, 16 / C);
+      // the multi-wave variant: as many waves per category as a 1024-thread
+      // workgroup holds (<= 4), fewer when that schedule's hand-off slots
+      // overflow LDS (a balanced 64-taxon tree at C = 4: 3 waves)
       QmwPlan mp;
-      if (W >= 2 && quad_mw_plan(c->prog, qp, c->nsteps, W, mp)) {
+      for (int W = std::min(QMW_MAXW, 16 / C); W >= 2 && !c->qmw_ok; --W) {
+        if (!quad_mw_plan(c->prog, qp, c->nsteps, W, mp)) continue;
         const size_t lds = qmw_lds_bytes(S, C, c->nmat, c->R, mp.nslot);
         if (lds + EIG_LEN * sizeof(double) <= LDS_CAP) {
           TRY_C(dalloc(&c->d_mprog, mp.prog.size()));

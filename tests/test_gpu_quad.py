@@ -165,7 +165,7 @@ def test_quad_epilogue_handoffs_stress_bitwise(name, monkeypatch):
 
 
 @pytest.mark.parametrize("name", ["fluA", "HCV", "DS1", "rand_C1_JC", "rand_C3_GTR", "unrooted_C5", "many_blocks",
-                                  "caterpillar", "balanced"])
+                                  "caterpillar", "balanced", "balanced64", "balanced128"])
 @pytest.mark.parametrize("n", [1, 4, 16])
 def test_quad_multiwave_rows_bitwise_equal_one_wave(name, n, monkeypatch):
     """The multi-wave quad sweep (qmw_kernel: the post-order program split
@@ -174,7 +174,14 @@ def test_quad_multiwave_rows_bitwise_equal_one_wave(name, n, monkeypatch):
     and writes every dL/dP entry from the one wave owning its step: the rows,
     site log-likelihoods included, are bitwise PHY_QMW=0's."""
     make = {"caterpillar": lambda: cases.random_case(305, S=40, P=300, C=4, model="GTR", caterpillar=True),
-            "balanced": lambda: cases.random_case(306, S=32, P=400, C=4, model="HKY")}.get(name, CASES.get(name))
+            "balanced": lambda: cases.random_case(306, S=32, P=400, C=4, model="HKY"),
+            # these two overflowed LDS with four waves per category and fell back to one wave (r05): the
+            # plan now takes the most waves whose hand-off slots fit beside the matrix records (one-hot
+            # and all-ones tips, as the reference's data: R = 5 record vectors; five more ambiguity
+            # masks would make R = 9 and the 64-taxon records alone 145 KB of the 160)
+            "balanced64": lambda: cases.random_case(306, S=64, P=400, C=4, model="HKY", ambiguous=0.0),
+            "balanced128": lambda: cases.random_case(307, S=128, P=300, C=2, model="HKY", ambiguous=0.0),
+            }.get(name, CASES.get(name))
     case = make()
     bl, mv = _draws(case, n, 41)
     out = {}
@@ -184,8 +191,8 @@ def test_quad_multiwave_rows_bitwise_equal_one_wave(name, n, monkeypatch):
         plan = eng.quad_plan()
         if qmw == "0":
             assert plan["waves"] == 1 and plan["span"] == case.S - 1
-        elif name in ("fluA", "HCV", "DS1", "balanced"):  # (the plan falls back to one wave when its
-            # records and hand-off slots overflow LDS; a caterpillar has nothing to run side by side)
+        elif name in ("fluA", "HCV", "DS1", "balanced", "balanced64", "balanced128"):  # (a caterpillar has
+            # nothing to run side by side)
             assert plan["waves"] >= 2 and plan["span"] < 0.75 * (case.S - 1), plan
         out[qmw] = eng.evaluate_rows(bl, mv)
         if n == 1:
