@@ -604,31 +604,47 @@ __device__ void qgrad_body(const QgArgs& a, int draw, int tid, double* sh, const
   for (int vw = wave; vw < QG_THREADS / 64; vw += nwr) {  // virtual wave vw: threads vw*64 + lane
     const int vt = vw * 64 + lane;
     double m[4] = {0.0, 0.0, 0.0, 0.0};
-    for (int idx = vt >> 2; idx < C * B; idx += QG_THREADS / 4) {
-      const int c = idx / B, b = idx - c * B;
-      const double t = mdl[10 + c] * bl[b];
-      double g[4];  // row k of G; G[i][j] = row i's g[j], broadcast from lane i of the quad
-      getG(idx, k, g);
-      const double Ek = exp(slam[k] * t);
-      double E[4];
-      E[0] = dpp_d<0x00>(Ek);
-      E[1] = dpp_d<0x55>(Ek);
-      E[2] = dpp_d<0xAA>(Ek);
-      E[3] = dpp_d<0xFF>(Ek);
-      double T[4];  // row k of V^T G
+    // two items per trip, their loads and exps side by side (the
+    // accumulation stays in item order: the same bits as one at a time)
+    constexpr int QS = QG_THREADS / 4;
+    for (int idx = vt >> 2; idx < C * B; idx += 2 * QS) {
+      const bool two = idx + QS < C * B;  // (quad-uniform)
+      double t2[2], Ek2[2], g2[2][4];
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const double g0 = dpp_d<0x00>(g[j]), g1 = dpp_d<0x55>(g[j]), g2 = dpp_d<0xAA>(g[j]), g3 = dpp_d<0xFF>(g[j]);
-        T[j] = fma(sV[12 + k], g3, fma(sV[8 + k], g2, fma(sV[4 + k], g1, fma(sV[k], g0, 0.0))));
+      for (int h = 0; h < 2; ++h) {
+        const int ix = h && two ? idx + QS : idx;
+        const int c = ix / B, b = ix - c * B;
+        t2[h] = mdl[10 + c] * bl[b];
+        getG(ix, k, g2[h]);  // row k of G; G[i][j] = row i's g[j], broadcast from lane i of the quad
       }
 #pragma unroll
-      for (int l = 0; l < 4; ++l) {
-        double hh = 0.0;  // (V^T G V^-T)[k][l]
+      for (int h = 0; h < 2; ++h) Ek2[h] = exp(slam[k] * t2[h]);
 #pragma unroll
-        for (int j = 0; j < 4; ++j) hh = fma(T[j], sVi[l * 4 + j], hh);
-        const double ri = srinv[k * 4 + l];
-        const double phi = ri == 0.0 ? t * Ek : (Ek - E[l]) * ri;
-        m[l] = fma(hh, phi, m[l]);
+      for (int h = 0; h < 2; ++h) {
+        if (h && !two) break;
+        const double t = t2[h], Ek = Ek2[h];
+        const double(&g)[4] = g2[h];
+        double E[4];
+        E[0] = dpp_d<0x00>(Ek);
+        E[1] = dpp_d<0x55>(Ek);
+        E[2] = dpp_d<0xAA>(Ek);
+        E[3] = dpp_d<0xFF>(Ek);
+        double T[4];  // row k of V^T G
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const double g0 = dpp_d<0x00>(g[j]), g1 = dpp_d<0x55>(g[j]), gg2 = dpp_d<0xAA>(g[j]),
+                       g3 = dpp_d<0xFF>(g[j]);
+          T[j] = fma(sV[12 + k], g3, fma(sV[8 + k], gg2, fma(sV[4 + k], g1, fma(sV[k], g0, 0.0))));
+        }
+#pragma unroll
+        for (int l = 0; l < 4; ++l) {
+          double hh = 0.0;  // (V^T G V^-T)[k][l]
+#pragma unroll
+          for (int j = 0; j < 4; ++j) hh = fma(T[j], sVi[l * 4 + j], hh);
+          const double ri = srinv[k * 4 + l];
+          const double phi = ri == 0.0 ? t * Ek : (Ek - E[l]) * ri;
+          m[l] = fma(hh, phi, m[l]);
+        }
       }
     }
     // sum over the wave's 16 quads (lane bits 2..5): lanes with bits 2, 3
@@ -680,6 +696,23 @@ __device__ void qgrad_body(const QgArgs& a, int draw, int tid, double* sh, const
 // Register budget: K=2 targets two waves per SIMD (<= 256 VGPRs), K=1 four.
 // DL: the deep stack lives in LDS (no VMEM traffic or prefetch for it),
 // else in the per-workgroup global region behind a buffer descriptor.
+#ifdef PHY_STEPTIME
+// Diagnostic build only (tools/steptime.py): the shader clock (s_memtime) of
+// lane 0 of every category wave of draws [TT_DRAW0, TT_DRAW0 + TT_DRAWS) at
+// each program step and phase boundary, one slot per event.
+#ifndef TT_DRAW0
+#define TT_DRAW0 0
+#endif
+constexpr int TT_DRAWS = 64, TT_EV = 1024;
+__device__ unsigned long long g_tt[TT_DRAWS * 16][TT_EV];
+#define TT_MARK(i)                                                                   \
+  do {                                                                               \
+    if (draw >= TT_DRAW0 && draw < TT_DRAW0 + TT_DRAWS && lane == 0)                 \
+      g_tt[(draw - TT_DRAW0) * 16 + wv][(i)] = __builtin_amdgcn_s_memtime();         \
+  } while (0)
+#else
+#define TT_MARK(i) do {} while (0)
+#endif
 #ifndef PHY_WPE2
 #define PHY_WPE2 2  // waves per SIMD the K=2 kernel is register-budgeted for
 #endif
@@ -846,6 +879,7 @@ __global__ void __launch_bounds__(MAXT) __attribute__((amdgpu_waves_per_eu(MAXT 
   const int trips = (a.nblk - vg + VG - 1) / VG;
   for (int trip = 0; trip < trips; ++trip) {
     const int blk = vg + trip * VG;
+    TT_MARK(trip * 320 + 0);
 #pragma unroll
     for (int k = 0; k < K; ++k) lofs[k] = (blk * WAVE * K + k * WAVE + lane < a.P) ? lcol[k] : OOB;
     __syncthreads();  // the previous block's tip / root-exchange reads are done
@@ -874,6 +908,7 @@ __global__ void __launch_bounds__(MAXT) __attribute__((amdgpu_waves_per_eu(MAXT 
     }
     __syncthreads();
     WAIT_VMCNT0();
+    TT_MARK(trip * 320 + 1);
 
     // ------------------------------ forward ------------------------------
     // Step s: a_y = P t_y (tip) or top; a_x = P t_x (tip), top (y a tip) or
@@ -955,12 +990,15 @@ __global__ void __launch_bounds__(MAXT) __attribute__((amdgpu_waves_per_eu(MAXT 
       for (int k = 0; k < K; ++k) dA[k] = {0.0, 0.0, 0.0, 0.0};  // step 0 has no internal child
       Step sA = ld_step<K == 2>(prog, 0), sB;
       for (int s = 0;;) {
+        TT_MARK(trip * 320 + 2 + s);
         FSTEP(s, dA, dB, sA, sB);
         if (++s >= nsteps) break;
+        TT_MARK(trip * 320 + 2 + s);
         FSTEP(s, dB, dA, sB, sA);
         if (++s >= nsteps) break;
       }
     }
+    TT_MARK(trip * 320 + 152);
 
     // ------------------------- root / site log L -------------------------
     // (the C category waves exchange through their tails)
@@ -978,6 +1016,7 @@ __global__ void __launch_bounds__(MAXT) __attribute__((amdgpu_waves_per_eu(MAXT 
       for (int cc = 0; cc < C; ++cc) L[k] += tail0[(size_t)cc * tstride + k * WAVE + lane];
     }
     __syncthreads();  // every wave has read the exchange before deep entries are rewritten
+    TT_MARK(trip * 320 + 153);
     V4 topr[K];
 #pragma unroll
     for (int k = 0; k < K; ++k) {
@@ -1168,15 +1207,18 @@ __global__ void __launch_bounds__(MAXT) __attribute__((amdgpu_waves_per_eu(MAXT 
       CSet A, Bs;
       LOAD_SET(s, A);
       for (;;) {
+        TT_MARK(trip * 320 + 154 + (nsteps - 1 - s));
         LOAD_SET(s - 1, Bs);
         RSTEP(s, A, Bs);
         if (--s < 0) break;
+        TT_MARK(trip * 320 + 154 + (nsteps - 1 - s));
         LOAD_SET(s - 1, A);
         RSTEP(s, Bs, A);
         if (--s < 0) break;
       }
     }
     WAIT_VMCNT0();
+    TT_MARK(trip * 320 + 310);
     gfirst = false;
   }
 
@@ -1207,6 +1249,7 @@ __global__ void __launch_bounds__(MAXT) __attribute__((amdgpu_waves_per_eu(MAXT 
     // fin: the finalize runs here; its LDS (inner products [C][B], then the
     // waves' scalar partials [C][8], then qgrad's) reuses the sweep's, once
     // every wave is done
+    TT_MARK(990);
     double* innerL = mats0;
     double* scalL = mats0 + (size_t)C * a.B;
     if (a.fin) __syncthreads();
@@ -1237,11 +1280,14 @@ __global__ void __launch_bounds__(MAXT) __attribute__((amdgpu_waves_per_eu(MAXT 
       for (int u = 0; u < U; ++u) {
         const int k = k0 + u * WAVE;
         if (k < tot) {
+          // the 16-entry butterfly (xor 8, 4, 2, 1) in DPP: after the first
+          // stage lanes i and i^8 hold the same sum, so row_ror:4 reads the
+          // value xor 4 would -- the __shfl_xor butterfly's bits, no LDS trips
           double sv = g[u] * qp[u];
-          sv += __shfl_xor(sv, 8, 16);
-          sv += __shfl_xor(sv, 4, 16);
-          sv += __shfl_xor(sv, 2, 16);
-          sv += __shfl_xor(sv, 1, 16);
+          sv += dpp_d<DPP_ROW_ROR8>(sv);
+          sv += dpp_d<0x124>(sv);  // row_ror:4
+          sv += dpp_d<DPP_QUAD_XOR2>(sv);
+          sv += dpp_d<DPP_QUAD_XOR1>(sv);
           gout[((size_t)c * a.B + bb[u]) * 16 + e16] = g[u];
           if (e16 == 0) {
             inner_d[(size_t)c * a.B + bb[u]] = sv;
@@ -1250,6 +1296,7 @@ __global__ void __launch_bounds__(MAXT) __attribute__((amdgpu_waves_per_eu(MAXT 
         }
       }
     }
+    TT_MARK(991);
     if (a.fin) {
       if (lane == 0) {
         double* sl = scalL + (size_t)wv * 8;
@@ -1287,6 +1334,7 @@ __global__ void __launch_bounds__(MAXT) __attribute__((amdgpu_waves_per_eu(MAXT 
           out[1 + B + 2 * C + q] = t;
         }
       }
+      TT_MARK(992);
       if (a.qfused) {  // the Q-parameter chain rule (qgrad_kernel's work, same bits)
         double* qsh = scalL + (size_t)C * 8;
         const QgArgs q{a.eig, a.model, a.blens, a.grows, a.grows_stride, a.out, a.outlen, C, B, a.kind};
@@ -1295,6 +1343,7 @@ __global__ void __launch_bounds__(MAXT) __attribute__((amdgpu_waves_per_eu(MAXT 
       }
     }
   }
+  TT_MARK(1000);
 }
 
 #include "quad_engine.inc"
@@ -3393,6 +3442,14 @@ int phy_create_multi(int S, int P, int C, int rooted, int model, const uint8_t* 
   *out = c;
   return PHY_OK;
 }
+
+#ifdef PHY_STEPTIME
+extern "C" int phy_debug_steptime(unsigned long long* out) {  // diagnostic build only (tools/steptime.py)
+  HIP_TRY(hipDeviceSynchronize());
+  HIP_TRY(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_tt), sizeof(g_tt)));
+  return PHY_OK;
+}
+#endif
 
 int phy_destroy(phy_ctx* ctx) {
   free_ctx(ctx);

@@ -43,13 +43,15 @@ step_parity() {  # the parity suites of the pattern sweep (every plan) and the c
   tail -15 $O/pytest_parity.log
 }
 vname() {  # file-name tag of a variant spec
-  case $1 in base) echo base ;; *.so) basename $1 .so ;; *) echo "$1" | tr ',=/' '__-' ;; esac
+  case $1 in base) echo base ;; *.so) basename $1 .so ;; *.so:*) echo "$(basename ${1%%:*} .so)_$(echo ${1#*:} | tr ',=/' '__-')" ;;
+    *) echo "$1" | tr ',=/' '__-' ;; esac
 }
-vrun() {  # vrun SPEC cmd... : the command under that variant
+vrun() {  # vrun SPEC cmd... : the command under that variant (SPEC: base, x.so, x.so:K=V[,K=V], K=V[,K=V])
   local v=$1; shift
   case $v in
     base) "$@" ;;
     *.so) PHYLO_HIP_AB=1 PHYLO_HIP_LIB=$PWD/$v "$@" ;;
+    *.so:*) env $(echo "${v#*:}" | tr ',' ' ') PHYLO_HIP_AB=1 PHYLO_HIP_LIB=$PWD/${v%%:*} "$@" ;;
     *) env $(echo "$v" | tr ',' ' ') "$@" ;;
   esac
 }
