@@ -803,7 +803,7 @@ def main():
             sampler[name + "_us_per_call_1draw"] = 1e6 * (time.perf_counter() - ta) / 300
             lk.close()
             lk = sampler_ctx(name, 100)
-            for _ in range(5):
+            for _ in range(20):
                 lk.evaluate_rows(bl100, mv100)
             ta = time.perf_counter()
             for _ in range(100):
