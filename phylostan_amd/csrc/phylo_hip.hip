@@ -272,11 +272,6 @@ __device__ __forceinline__ int reduce16_entry(int lane) {
 // ---------------------------------------------------------------------------
 // kernel arguments
 // ---------------------------------------------------------------------------
-#ifndef PHY_DBUF
-#define PHY_DBUF 0
-#endif
-constexpr int CLO_MAX = 16;  // chunks per pass whose next staging the sweep issues ahead (PHY_DBUF)
-
 struct SweepArgs {
   const uint8_t* tips;    // [S][Ppad/2] tip nibbles: record vector index, pattern 2j+1 in the high nibble
   const double* weights;  // [Ppad]   (0 on padding)
@@ -301,10 +296,6 @@ struct SweepArgs {
   // qfused (fin only): the Q-parameter chain rule (qgrad_kernel's work,
   // qgrad_body) runs after the finalize, in the same workgroup
   int qfused, kind;
-  // the LDS chunk plan (PHY_DBUF): chunk k holds matrices [clo[k], clo[k+1]);
-  // nch = 0: no table (the staging of the next chunk is not issued ahead)
-  int nch;
-  int clo[CLO_MAX + 1];
 };
 
 // LDS carve (16-B aligned pieces), K columns per lane:
@@ -378,19 +369,6 @@ __device__ __forceinline__ void st_v4(__amdgpu_buffer_rsrc_t srd, uint32_t off, 
 // wait would be invisible to it): clears loads left pending by staging
 // loops so the step loops are not charged a loop-carried vmcnt(0).
 #define WAIT_VMCNT0() __builtin_amdgcn_s_waitcnt(0x0F70)
-
-// One LDS-DMA piece: 64 lanes x 16 B from each lane's `gsrc` to the LDS
-// bytes [lds_dst, lds_dst + 1 KiB) (lane l at lds_dst + 16 l).  M0 is written
-// and restored inside the statement (the compiler keeps its own use of it).
-// hipcc does not count it: the issuing wave waits with its own vmcnt before
-// reading the bytes.
-__device__ __forceinline__ void glds16(const void* gsrc, uint32_t lds_dst) {
-  unsigned keep;
-  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
-               : "=&s"(keep)
-               : "v"(gsrc), "s"(lds_dst)
-               : "memory");
-}
 
 // Matrix records (pmat_kernel): R 4-vectors per matrix -- the four columns
 // of P, then P t for every non-one-hot tip mask t present in the data (the
@@ -832,49 +810,7 @@ __global__ void __launch_bounds__(MAXT) __attribute__((amdgpu_waves_per_eu(MAXT 
 
   // ---- this wave's chunk of matrix records in LDS (no barrier: private) ----
   int cur = -1, m0 = 0;
-#if PHY_DBUF
-  // Two buffers of half = cap_m / 2 records each (the host plans chunks of at
-  // most half): chunk k lives in buffer k & 1.  On entering chunk k the wave
-  // issues the LDS-DMA of the next chunk of the pass (k + dir) into the other
-  // buffer, whose chunk is done, so a later switch finds it landed instead of
-  // waiting one staging round trip behind the stores in flight.
-  const int half = a.cap_m / 2;
-  int res0 = -1, res1 = -1;  // chunk resident in (or on its way to) each buffer
-  bool pend = false;         // a DMA may be in flight
-  double* matsc = mats;      // the current chunk's buffer
-  auto dma_chunk = [&](int lo, int n, int b) {
-    const char* src = reinterpret_cast<const char*>(pmat_c + (size_t)lo * rec) + lane * 16;
-    const uint32_t dst =
-        __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(mats + (size_t)b * half * rec));
-    const int bytes = n * rec * 8;
-    for (int off = 0; off < bytes; off += WAVE * 16)  // (wave-uniform; the last piece's tail lanes idle)
-      if (off + lane * 16 < bytes) glds16(src + off, dst + off);
-    pend = true;
-  };
-  auto ensure_chunk = [&](const Step& st, int dir) {
-    const int ch = st.ch;
-    if (ch == cur) return;  // wave-uniform
-    const int b = ch & 1;
-    if ((b ? res1 : res0) != ch) {
-      dma_chunk(st.m0, st.mn, b);
-      if (b) res1 = ch; else res0 = ch;
-    }
-    if (pend) {  // this chunk's DMA (issued ahead, or just now) has landed
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      pend = false;
-    }
-    cur = ch;
-    m0 = st.m0;
-    matsc = mats + (size_t)b * half * rec;
-    const int nx = ch + dir;
-    if (nx >= 0 && nx < a.nch && ((nx & 1) ? res1 : res0) != nx) {
-      dma_chunk(a.clo[nx], a.clo[nx + 1] - a.clo[nx], nx & 1);
-      if (nx & 1) res1 = nx; else res0 = nx;
-    }
-  };
-  auto mrec = [&](int m) __attribute__((always_inline)) -> const double* { return matsc + (size_t)(m - m0) * rec; };
-#else
-  auto ensure_chunk = [&](const Step& st, int) {
+  auto ensure_chunk = [&](const Step& st) {
     const int ch = st.ch;
     if (ch == cur) return;  // wave-uniform
     const int lo = st.m0, n = st.mn;
@@ -899,7 +835,6 @@ __global__ void __launch_bounds__(MAXT) __attribute__((amdgpu_waves_per_eu(MAXT 
     m0 = lo;
   };
   auto mrec = [&](int m) __attribute__((always_inline)) -> const double* { return mats + (size_t)(m - m0) * rec; };
-#endif
   // record index of tip t, column k: a nibble (two lanes share a byte)
   auto tipb = [&](int t, int k) __attribute__((always_inline)) -> unsigned {
     return (tipl[(t * K + k) * (WAVE / 2) + (lane >> 1)] >> ((lane & 1) * 4)) & 15u;
@@ -995,7 +930,7 @@ __global__ void __launch_bounds__(MAXT) __attribute__((amdgpu_waves_per_eu(MAXT 
       _Pragma("unroll")                                                                                               \
         for (int k = 0; k < K; ++k) dnext[k] = ld_v4(srd_scr, lofs[k] + ent(need, sn.xs), half_bytes);         \
       }                                                                                                               \
-      ensure_chunk(st, 1);                                                                                            \
+      ensure_chunk(st);                                                                                               \
       const int x = st.x, y = st.y, fl = st.fl, vs = st.vs;                        \
       V4 ax[K], ay[K], pv[K];                                                                                         \
       if (y >= 0) {                                                                                                   \
@@ -1171,7 +1106,7 @@ __global__ void __launch_bounds__(MAXT) __attribute__((amdgpu_waves_per_eu(MAXT 
     } while (0)
     #define RSTEP_V(s, cs, cn, XT, YT) do {                                               \
       const Step& st = cs.st;                                                     \
-      ensure_chunk(st, -1);                                                       \
+      ensure_chunk(st);                                                           \
       const int fl = st.fl;                                                       \
       V4 rv[K], ax[K], ay[K], q[K], rx[K], ry[K];                                 \
       unsigned bx[K], by[K];                                                      \
@@ -2303,7 +2238,6 @@ struct phy_ctx {
   long qscr_wgs = 0;
   bool qfuse_pref = true;      // Q-parameter chain rule inside the sweep (PHY_QFUSE=0: off)
   int cap_m = 0, nchunks = 0;  // current LDS plan
-  std::vector<int> clo;        // its chunk boundaries (nchunks + 1)
   int deep_pref = 0;           // deep stack: 0 automatic, 1 LDS, 2 global
   bool deep_lds = false;       // current plan keeps the whole deep stack in LDS
   int ndl = 0;                 // deep entries in LDS (== ndeep when deep_lds)
@@ -2684,11 +2618,10 @@ int plan_chunks(phy_ctx* c) {
   // run of steps whose matrices fit
   int used = 0, ch = 0, lo = 0;
   std::vector<int> first_step{0};
-  const int ccap = PHY_DBUF ? cap / 2 : cap;  // (PHY_DBUF: two buffers of cap / 2)
   for (int s = 0; s < c->nsteps; ++s) {
     const int* p = &c->prog[(size_t)s * STEP_INTS];
     const int n = (p[ST_MX] >= 0) + (p[ST_MY] >= 0) + (p[ST_MV] >= 0);
-    if (used + n > ccap) {
+    if (used + n > cap) {
       first_step.push_back(s);
       lo += used;
       used = 0;
@@ -2741,9 +2674,6 @@ int plan_chunks(phy_ctx* c) {
   }
   c->cap_m = cap;
   c->nchunks = ch + 1;
-  c->clo.assign(1, 0);  // chunk k: matrices [clo[k], clo[k+1])
-  for (int k = 1; k <= ch; ++k) c->clo.push_back(c->prog[(size_t)first_step[k] * STEP_INTS + ST_M0]);
-  c->clo.push_back(c->nmat);
   c->deep_lds = ndl > 0 && ndl == c->ndeep;
   c->ndl = ndl;
   return PHY_OK;
@@ -3086,8 +3016,6 @@ int launch_pattern(phy_ctx* ctx, int n, const double* d_blens, const double* d_m
                ctx->nslots,  ctx->ndeep,   ctx->ndl,     ctx->nblk,    ctx->nmat,    ctx->R,         ctx->cap_m,
                B,            phy_output_len(ctx), g_direct, ctx->extra, fin, d_blens, grows, gstride,
                qf,           ctx->kind};
-  sa.nch = ctx->nchunks <= CLO_MAX ? ctx->nchunks : 0;
-  for (int k = 0; k <= CLO_MAX; ++k) sa.clo[k] = k < (int)ctx->clo.size() ? ctx->clo[k] : 0;
   hipEvent_t e0 = nullptr, e1 = nullptr;
   if (ctx->timing) {
     int rc = timing_begin(ctx, st, &e0, &e1);
