@@ -125,8 +125,9 @@ int phy_class_fused(const phy_ctx* ctx, int* level_pairs, int* chunk_spans);
 
 /* The sampler's small-call sweep (calls of <= 16 draws, the quad sweep):
  * waves per category (0: the quad sweep does not apply to this context, 1:
- * the one-wave quad sweep, 2-4: the multi-wave form, whose host list-schedule
- * splits the post-order program over that many waves with LDS hand-offs),
+ * the one-wave quad sweep, 2 up to 16 / C: the multi-wave form, whose host
+ * list-schedule splits the post-order program over that many waves with LDS
+ * hand-offs -- the most waves whose hand-off slots still fit LDS),
  * the schedule's length in program steps (the one-wave sweep: every step),
  * and its LDS hand-off slots.  PHY_QMW=0 at phy_create keeps the one-wave
  * form; the rows are bitwise the same either way. */
