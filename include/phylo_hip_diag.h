@@ -111,8 +111,8 @@ int phy_class_clades(const phy_ctx* ctx, int* fused_levels, int* clades, long lo
  */
 int phy_class_chain(const phy_ctx* ctx, int* levels, int* lowest, int* top_classes);
 
-/* Launch fusions of the class sweep's level launches, both bitwise the
- * unfused values (read at phy_create):
+/* Launch fusions and layouts of the class sweep's level launches, all
+ * bitwise the unfused / default values (read at phy_create):
  *   level_pairs   forward level pairs -- adjacent levels (above the fused
  *                 clade levels, below the top chain) in one launch, the upper
  *                 level recomputing its children of the level below from
@@ -120,8 +120,13 @@ int phy_class_chain(const phy_ctx* ctx, int* levels, int* lowest, int* top_class
  *                 levels of at most n classes (default: no cap).
  *   chunk_spans   long tile-crossing segments summed by the reverse chunk
  *                 of their class (the whole wave), so those levels have no
- *                 FIX launch.  PHY_REVFIX=0: none. */
-int phy_class_fused(const phy_ctx* ctx, int* level_pairs, int* chunk_spans);
+ *                 FIX launch.  PHY_REVFIX=0: none.
+ *   parent_order_levels  levels whose secondary children's staging is
+ *                 written in the parent's class order and gathered by the
+ *                 RED tiles through a permutation (levels staging at least
+ *                 100,000 classes; PHY_STAGE_ORDER=n sets that threshold,
+ *                 0: every level above the clades). */
+int phy_class_fused(const phy_ctx* ctx, int* level_pairs, int* chunk_spans, int* parent_order_levels);
 
 /* The sampler's small-call sweep (calls of <= 16 draws, the quad sweep):
  * waves per category (0: the quad sweep does not apply to this context, 1:

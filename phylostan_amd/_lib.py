@@ -62,7 +62,7 @@ SIGNATURES = {
     "phy_class_clades": (ctypes.c_int, [ctypes.c_void_p, _c_int_p, _c_int_p, ctypes.POINTER(ctypes.c_longlong)]),
     "phy_class_chain": (ctypes.c_int, [ctypes.c_void_p, _c_int_p, _c_int_p, _c_int_p]),
     "phy_quad_plan": (ctypes.c_int, [ctypes.c_void_p, _c_int_p, _c_int_p, _c_int_p]),
-    "phy_class_fused": (ctypes.c_int, [ctypes.c_void_p, _c_int_p, _c_int_p]),
+    "phy_class_fused": (ctypes.c_int, [ctypes.c_void_p, _c_int_p, _c_int_p, _c_int_p]),
 }
 
 

@@ -3796,11 +3796,12 @@ int phy_class_chain(const phy_ctx* ctx, int* levels, int* lowest, int* top_class
   return PHY_OK;
 }
 
-int phy_class_fused(const phy_ctx* ctx, int* level_pairs, int* chunk_spans) {
+int phy_class_fused(const phy_ctx* ctx, int* level_pairs, int* chunk_spans, int* parent_order_levels) {
   if (!ctx) return fail(PHY_EINVAL, "NULL ctx");
-  if (ctx->ms) return phy_class_fused(ctx->ms->shard[0], level_pairs, chunk_spans);
+  if (ctx->ms) return phy_class_fused(ctx->ms->shard[0], level_pairs, chunk_spans, parent_order_levels);
   if (level_pairs) *level_pairs = ctx->ce ? ctx->ce->npairs : 0;
   if (chunk_spans) *chunk_spans = ctx->ce ? ctx->ce->nclong : 0;
+  if (parent_order_levels) *parent_order_levels = ctx->ce ? ctx->ce->nsord : 0;
   return PHY_OK;
 }
 

@@ -330,13 +330,14 @@ class TreeLikelihood:
         cl, clo, ctop = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
         _lib.check(self.lib.phy_class_chain(self.ctx, ctypes.byref(cl), ctypes.byref(clo), ctypes.byref(ctop)),
                    "phy_class_chain")
-        pr, cs = ctypes.c_int(), ctypes.c_int()
-        _lib.check(self.lib.phy_class_fused(self.ctx, ctypes.byref(pr), ctypes.byref(cs)), "phy_class_fused")
+        pr, cs, po = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
+        _lib.check(self.lib.phy_class_fused(self.ctx, ctypes.byref(pr), ctypes.byref(cs), ctypes.byref(po)),
+                   "phy_class_fused")
         return dict(classes=ll[0].value, levels=ii[0].value, root_classes=ii[1].value, stage=ll[1].value,
                     staged=ll[2].value, tiles=ii[2].value, spans=ii[3].value, clade_levels=fl.value,
                     clades=nc.value, clade_max=big.value, chain_levels=cl.value, chain_lowest=clo.value,
                     chain_top_classes=ctop.value, level_pairs=pr.value,
-                    chunk_spans=cs.value)
+                    chunk_spans=cs.value, parent_order_levels=po.value)
 
     def quad_plan(self):
         """The small-call sweep's plan: waves per category, schedule length in

@@ -399,3 +399,44 @@ def test_class_root_chain_bitwise_equal_to_chain_forward_launch(make, monkeypatc
     bl = case.blens[None, :] * rng.uniform(0.8, 1.2, (3, case.blens.size))
     mv = np.repeat(case.model_vec()[None], 3, axis=0)
     assert np.array_equal(fused.evaluate_rows(bl, mv), plain.evaluate_rows(bl, mv))
+
+
+@pytest.mark.parametrize("make", [cases.fluA_case, cases.hcv_case, "rep", "rep_nochain", "deep", "syn200k"],
+                         ids=["fluA", "HCV_chain", "repetitive", "repetitive_no_chain", "random300", "synthetic200k"])
+def test_class_parent_order_staging_bitwise_equal(make, monkeypatch):
+    """Secondary-child staging written in the parent's class order and
+    gathered by the RED tiles through the staging permutation (every level
+    above the clades: PHY_STAGE_ORDER=0) against every contribution stored at
+    its reduction position (PHY_STAGE_ORDER above any level's staging): the
+    same values reduced in the same order -- every output bitwise equal,
+    batched draws too, and at the parity bar against the oracle.  Covers the
+    chain externals of a parent-order level (written by the chain reverse at
+    their reduction positions: the permutation's identity entries)."""
+    if make == "syn200k":
+        from phylostan_amd import synthetic
+        pd, prm = synthetic.simulate(n_sites=200_000)
+        case = cases.Case("syn200k", pd.tipcodes, pd.weights, pd.peel0, True, "GTR", 4, prm["blens"], prm["freqs"],
+                          prm["rates"], prm["rs"], prm["ps"])
+    elif make in ("rep", "rep_nochain"):
+        case = _repetitive_case()
+        if make == "rep_nochain":
+            monkeypatch.setenv("PHY_CHAIN", "0")
+    elif make == "deep":
+        case = cases.random_case(9, S=300, P=500, C=4, model="GTR", rooted=True)
+    else:
+        case = make()
+    monkeypatch.setenv("PHY_STAGE_ORDER", str(1 << 40))
+    plain = _class_engine(case, max_draws=3)
+    monkeypatch.setenv("PHY_STAGE_ORDER", "0")
+    porder = _class_engine(case, max_draws=3)
+    monkeypatch.delenv("PHY_STAGE_ORDER")
+    assert plain.class_info()["parent_order_levels"] == 0
+    assert porder.class_info()["parent_order_levels"] >= 1, porder.class_info()
+    a = porder.evaluate(case.blens, case.model_vec(), site_ll=True)
+    b = plain.evaluate(case.blens, case.model_vec(), site_ll=True)
+    _assert_rows_equal(a, b)
+    check_case(case, porder, a)
+    rng = np.random.default_rng(14)
+    bl = case.blens[None, :] * rng.uniform(0.8, 1.2, (3, case.blens.size))
+    mv = np.repeat(case.model_vec()[None], 3, axis=0)
+    assert np.array_equal(porder.evaluate_rows(bl, mv), plain.evaluate_rows(bl, mv))
