@@ -402,7 +402,8 @@ def test_class_root_chain_bitwise_equal_to_chain_forward_launch(make, monkeypatc
 
 
 @pytest.mark.parametrize("make", [cases.fluA_case, cases.hcv_case, "rep", "rep_nochain", "deep", "syn200k"],
-                         ids=["fluA", "HCV_chain", "repetitive", "repetitive_no_chain", "random300", "synthetic200k"])
+                         ids=["fluA_no_chain", "HCV_chain", "repetitive", "repetitive_no_chain", "random300",
+                              "synthetic200k"])
 def test_class_parent_order_staging_bitwise_equal(make, monkeypatch):
     """Secondary-child staging written in the parent's class order and
     gathered by the RED tiles through the staging permutation (every level
@@ -412,19 +413,25 @@ def test_class_parent_order_staging_bitwise_equal(make, monkeypatch):
     batched draws too, and at the parity bar against the oracle.  Covers the
     chain externals of a parent-order level (written by the chain reverse at
     their reduction positions: the permutation's identity entries)."""
-    if make == "syn200k":
+    if make == "syn200k":  # (the automatic plan: clades, pairs, no chain)
         from phylostan_amd import synthetic
         pd, prm = synthetic.simulate(n_sites=200_000)
         case = cases.Case("syn200k", pd.tipcodes, pd.weights, pd.peel0, True, "GTR", 4, prm["blens"], prm["freqs"],
                           prm["rates"], prm["rs"], prm["ps"])
-    elif make in ("rep", "rep_nochain"):
-        case = _repetitive_case()
-        if make == "rep_nochain":
-            monkeypatch.setenv("PHY_CHAIN", "0")
-    elif make == "deep":
-        case = cases.random_case(9, S=300, P=500, C=4, model="GTR", rooted=True)
     else:
-        case = make()
+        # the small plans' levels above the bottom clades are mostly chain: no clades here, so the
+        # levels below the chain launch on their own (with secondary children and chain externals)
+        monkeypatch.setenv("PHY_CLADE", "0")
+        if make in ("rep", "rep_nochain"):
+            case = _repetitive_case()
+            if make == "rep_nochain":
+                monkeypatch.setenv("PHY_CHAIN", "0")
+        elif make == "deep":
+            case = cases.random_case(9, S=300, P=500, C=4, model="GTR", rooted=True)
+        else:
+            case = make()
+            if make is cases.fluA_case:
+                monkeypatch.setenv("PHY_CHAIN", "0")
     monkeypatch.setenv("PHY_STAGE_ORDER", str(1 << 40))
     plain = _class_engine(case, max_draws=3)
     monkeypatch.setenv("PHY_STAGE_ORDER", "0")
