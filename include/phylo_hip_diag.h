@@ -66,7 +66,7 @@ int phy_set_recompute(phy_ctx* ctx, int on);
 int phy_recomputed_partials(const phy_ctx* ctx);
 
 /* Engine: 1 = pattern sweep (one lane per pattern column; a call of at most
- * 16 draws takes its quad form -- a quad of lanes per column, matrix records
+ * 32 draws takes its quad form -- a quad of lanes per column, matrix records
  * built in the sweep when the eigensystems are host-formed, an epilogue split
  * over workgroups; PHY_QUAD=0 at phy_create keeps the column sweep), 2 = class sweep
  * (site repeats: the forward pass once per distinct tip-state tuple of each
@@ -128,7 +128,7 @@ int phy_class_chain(const phy_ctx* ctx, int* levels, int* lowest, int* top_class
  *                 0: every level above the clades). */
 int phy_class_fused(const phy_ctx* ctx, int* level_pairs, int* chunk_spans, int* parent_order_levels);
 
-/* The sampler's small-call sweep (calls of <= 16 draws, the quad sweep):
+/* The sampler's small-call sweep (calls of <= 32 draws, the quad sweep):
  * waves per category (0: the quad sweep does not apply to this context, 1:
  * the one-wave quad sweep, 2 up to 16 / C: the multi-wave form, whose host
  * list-schedule splits the post-order program over that many waves with LDS

@@ -271,7 +271,7 @@ class TreeLikelihood:
         self._st = None  # the staging rows follow the row length
 
     def set_engine(self, mode=0):
-        """0 automatic, 1 pattern sweep (its quad form for calls of <= 16
+        """0 automatic, 1 pattern sweep (its quad form for calls of <= 32
         draws), 2 class sweep (site repeats).  Round 3's resident class sweep
         (mode 3) is retired: phy_set_engine refuses it."""
         if isinstance(mode, str):
@@ -280,7 +280,7 @@ class TreeLikelihood:
 
     def prefer_latency_engine(self, probe=True, calls=24):
         """For host-driven samplers (a few draws per call, one call per
-        leapfrog / ELBO round): the pattern sweep (its quad form for <= 16
+        leapfrog / ELBO round): the pattern sweep (its quad form for <= 32
         draws) -- faster than round 3's resident class sweep on every
         workload (fluA 99.8 against 132 us per 4-draw call) -- unless the
         automatic choice is the class sweep (a large alignment); then both are

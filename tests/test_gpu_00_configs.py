@@ -339,7 +339,7 @@ def test_zero_rate_categories_vs_reference(k):
         assert all(v <= 1e-6 for v in fd.values()), (engine, fd)
         for key, v in list(fd.items()) + [("loglik", e_ll), ("site_ll", e_site), ("dLdP", e["dLdP"]), ("Q", eq)]:
             worst[key] = max(worst.get(key, 0.0), v)
-    # the batched device path (column sweep, one workgroup per draw): 32 draws, the point in every row
+    # a 32-draw batch (the quad sweep since round 6: calls of <= 32 draws), the point in every row
     n = 32
     eng = _engine(case, max_draws=n)
     rows = eng.evaluate_rows(np.repeat(case.blens[None], n, 0), np.repeat(case.model_vec()[None], n, 0))

@@ -1,5 +1,5 @@
 """GPU: the quad sweep (csrc/quad_engine.inc) -- the pattern engine's path
-for calls of <= 16 draws (a sampler's), a quad of lanes per (pattern,
+for calls of <= 32 draws (a sampler's), a quad of lanes per (pattern,
 category) column -- against the oracle and against the one / two column
 sweeps (PHY_QUAD=0), through the C-ABI.
 
@@ -54,7 +54,7 @@ def test_quad_single_eval_vs_oracle(name, monkeypatch):
 
 
 @pytest.mark.parametrize("name", ["fluA", "HCV", "DS1", "rand_C3_GTR", "unrooted_C5", "rand_C16_HKY", "many_blocks"])
-@pytest.mark.parametrize("n", [4, 16])
+@pytest.mark.parametrize("n", [4, 16, 32])
 def test_quad_batch_rows_equal_column_sweeps(name, n, monkeypatch):
     """The sampler's shape (host buffers, n draws per call, full rows):
     every row of the quad sweep against the one/two-column sweeps' row."""
@@ -166,7 +166,7 @@ def test_quad_epilogue_handoffs_stress_bitwise(name, monkeypatch):
 
 @pytest.mark.parametrize("name", ["fluA", "HCV", "DS1", "rand_C1_JC", "rand_C3_GTR", "unrooted_C5", "many_blocks",
                                   "caterpillar", "balanced", "balanced64", "balanced128"])
-@pytest.mark.parametrize("n", [1, 4, 16])
+@pytest.mark.parametrize("n", [1, 4, 16, 32])
 def test_quad_multiwave_rows_bitwise_equal_one_wave(name, n, monkeypatch):
     """The multi-wave quad sweep (qmw_kernel: the post-order program split
     over up to 4 waves per category by the host list-scheduler, LDS slot
