@@ -1959,8 +1959,9 @@ __global__ void __launch_bounds__(QG_THREADS) qgrad_kernel(FinArgs a) {
 constexpr int QFIN_THREADS = 256;
 constexpr int QFIN_ITEMS = QFIN_THREADS / 4;  // (c, b) items per workgroup
 constexpr int QFIN_SLOTS = 16;                // workgroup slots per draw it takes
-// HANDOFF.  The split epilogues (qfin_kernel, cls_epi_kernel) hand per-
-// workgroup partials to the draw's last-arriving workgroup inside one launch:
+// HANDOFF.  The sampler's split epilogue (qfin_kernel) hands per-
+// workgroup partials to the draw's last-arriving workgroup inside one launch
+// (the class sweep's epilogue did too until round 6; it is two launches now):
 // every hand-off byte is stored write-through (sc1: __hip_atomic_store
 // relaxed/agent), every storing wave drains vmcnt, a workgroup barrier, then
 // ONE lane's relaxed agent-scope ticket add; the workgroup whose add returns
@@ -2831,9 +2832,11 @@ int launch_class(phy_ctx* ctx, int n, const double* d_blens, const double* d_mod
                        (const int2*)e->d_gsub, e->d_gpsum, std::max(e->ngs, 1), e->nsub);
   EpiArgs ea{e->d_gpart, e->d_gbase, e->d_gcount, e->d_sslot, ctx->d_pmat, ctx->eig_cur, d_blens, d_model,
              ctx->d_gpos, grows, gstride, d_out, epi, epi + ncb, epi + 17 * ncb,
-             e->d_epicnt, C, B, ctx->nmat, ctx->R, std::max(e->ngs, 1), e->nrootch, phy_output_len(ctx), ctx->kind,
+             C, B, ctx->nmat, ctx->R, std::max(e->ngs, 1), e->nrootch, phy_output_len(ctx), ctx->kind,
              e->d_gpsum, e->d_pbase, std::max(e->nsub, 1)};
-  hipLaunchKernelGGL(cls_epi_kernel, dim3(C * B, n), dim3(EPI_THREADS), 0, st, ea);
+  // the per-item part (every workgroup resident at once), then the closing part
+  hipLaunchKernelGGL((cls_epi_kernel<EPI_WIDE_THREADS, 1>), dim3(C * B, n), dim3(EPI_WIDE_THREADS), 0, st, ea);
+  hipLaunchKernelGGL((cls_epi_kernel<EPI_THREADS, 2>), dim3(n), dim3(EPI_THREADS), 0, st, ea);
   *qdone = true;
   HIP_TRY(hipGetLastError());
   return PHY_OK;
@@ -3448,6 +3451,13 @@ int phy_create_multi(int S, int P, int C, int rooted, int model, const uint8_t* 
   return PHY_OK;
 }
 
+#ifdef PHY_EPITIME
+extern "C" int phy_debug_epitime(unsigned long long* out) {  // diagnostic build only (tools/epitime.py)
+  HIP_TRY(hipDeviceSynchronize());
+  HIP_TRY(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_et), sizeof(g_et)));
+  return PHY_OK;
+}
+#endif
 #ifdef PHY_STEPTIME
 extern "C" int phy_debug_steptime(unsigned long long* out) {  // diagnostic build only (tools/steptime.py)
   HIP_TRY(hipDeviceSynchronize());
