@@ -7,8 +7,8 @@ whole alignment) through a PHY_EPITIME build of the engine
 real-time clock (s_memrealtime, 100 MHz) of wave 0 of every epilogue
 workgroup of draw 0 at its phase boundaries -- per-item launch: 0 start,
 1 chunk-partial sums in LDS, 2 hand-offs stored; closing launch (last row):
-0 start, 4 hand-offs summed, 5 per-category sums done, 6 Q-parameter tail
-done.  Prints the phase durations (median / 90th percentile over the
+0 start, 3 M summed (wave 0), 7 branch sums, 4 barrier, 5 per-category sums
+done, 6 Q-parameter tail done.  Prints the phase durations (median / 90th percentile over the
 workgroups), how the workgroup starts spread over the launch, and the
 closing workgroup's timeline.  Diagnostic only.
 
@@ -64,8 +64,8 @@ def main():
     print("  workgroup starts: first %.2f, 25%% %.2f, 50%% %.2f, 75%% %.2f, last %.2f us" %
           (s[0], s[len(s) // 4], s[len(s) // 2], s[3 * len(s) // 4], s[-1]))
     print("  last hand-off stored %.2f us" % t[:, 2].max())
-    print("  closing workgroup: start %.2f, hand-offs summed %.2f, per-category %.2f, tail %.2f us" %
-          (close[0], close[4], close[5], close[6]))
+    print("  closing workgroup: start %.2f, M summed %.2f, branch sums %.2f, barrier %.2f, per-category %.2f, "
+          "tail %.2f us" % (close[0], close[3], close[7], close[4], close[5], close[6]))
     np.save(os.path.join(ROOT, "gpurun_out", "epitime.npy"), t)
 
 
